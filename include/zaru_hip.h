@@ -1,0 +1,131 @@
+/*
+ * zaru_hip.h -- C ABI of the MI355X (gfx950) CNN runner for Zaru's detection/landmark path.
+ *
+ * This is the drop-in boundary of SURVEY.md §8b: a fourth `Session` variant behind
+ * `ZARU_ONNX_BACKEND=hip`.  Every entry point names the reference interface it replaces
+ * (paths relative to placrosse/Zaru).  Conventions:
+ *   - every call returns ZR_OK (0) or a negative error class and sets a thread-local message
+ *     readable with zr_last_error() (reference: anyhow::Error from Loader::load /
+ *     NeuralNetwork::estimate, crates/zaru/src/nn/mod.rs:259, 450);
+ *   - no C++ exception or abort crosses this boundary;
+ *   - a session is safe to use from several threads at once (NeuralNetwork is Clone + Send +
+ *     Sync and HandTracker workers call estimate(&self) concurrently,
+ *     crates/zaru/src/hand/tracking.rs:165-181);
+ *   - tensors are f32, row-major, batch in dim 0 replacing the reference's fixed 1
+ *     (crates/zaru/src/nn/tensor.rs:19-34).
+ * The host side of the reference (Detector, Estimator, LandmarkTracker, ...) stays as is;
+ * INTEGRATION.md shows the Rust binding.
+ */
+#ifndef ZARU_HIP_H
+#define ZARU_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZR_OK 0
+#define ZR_ERR_INVALID_ARGUMENT (-1)
+#define ZR_ERR_MODEL (-2)       /* malformed ONNX, or an operator/pattern with no HIP lowering */
+#define ZR_ERR_DEVICE (-3)      /* HIP runtime failure (no GPU, out of memory, ...) */
+#define ZR_ERR_SHAPE (-4)       /* tensor count or shape mismatch */
+
+typedef struct zr_session zr_session; /* = Arc<NeuralNetworkImpl> (crates/zaru/src/nn/mod.rs:369-375) */
+
+/* A view of an image: RotatedRect in root-image coordinates (crates/zaru/src/image/mod.rs:
+ * 188-192), stored as the reference stores it: centre, size, clockwise radians. */
+typedef struct {
+    float cx, cy, w, h, rad;
+} zr_view;
+
+/* An RGBA8 frame (crates/zaru/src/image/mod.rs:47-51), r in the lowest byte. */
+typedef struct {
+    const uint8_t *rgba;
+    uint32_t width, height;
+    uint64_t row_stride; /* bytes */
+} zr_frame;
+
+/* NeuralNetwork::from_onnx(bytes)[.with_output_selection(sel)].load()
+ * (crates/zaru/src/nn/mod.rs:411, 247, 259-362).  `onnx` is only borrowed; weights are
+ * copied to the device.  n_sel == 0 selects every graph output. */
+int zr_session_create(const uint8_t *onnx, size_t len, const uint32_t *out_sel, size_t n_sel,
+                      int device, zr_session **out);
+
+/* Last Arc drop. */
+void zr_session_destroy(zr_session *s);
+
+/* num_inputs() / num_outputs() (crates/zaru/src/nn/mod.rs:416-423) */
+int zr_session_num_io(const zr_session *s, int is_output, size_t *n);
+
+/* inputs() / outputs() descriptors (crates/zaru/src/nn/mod.rs:428-443).  `shape` receives up
+ * to 8 dims with the batch dim = 1; `name` stays valid for the session's lifetime. */
+int zr_session_io(const zr_session *s, int is_output, size_t idx, const char **name,
+                  int64_t *shape, size_t *rank);
+
+/* NeuralNetwork::estimate (crates/zaru/src/nn/mod.rs:450-538), batched: `inputs[0]` is a
+ * host [batch,C,H,W] tensor, `outputs[i]` host buffers sized batch * per-image numel of
+ * output i.  Synchronous: returns with the outputs written. */
+int zr_session_run(zr_session *s, size_t batch, const float *const *inputs, size_t n_in,
+                   float *const *outputs, size_t n_out);
+
+/* Device-resident variant: `d_input` already in HBM ([batch,C,H,W]); outputs are device
+ * buffers; work is enqueued on `hip_stream` (NULL = default stream) and the call returns
+ * without waiting. */
+int zr_session_run_async(zr_session *s, size_t batch, const float *d_input, float *const *d_outputs,
+                         size_t n_out, void *hip_stream);
+
+/* Cnn::estimate (crates/zaru/src/nn/mod.rs:118-126) batched over views of one host RGBA8
+ * image: the image->tensor map (nn/mod.rs:54-73, ColorMapper::linear(lo..=hi)) runs on the
+ * GPU, bit-exact, and feeds the network directly.  Host outputs, synchronous. */
+int zr_cnn_estimate_views(zr_session *s, const uint8_t *rgba, uint32_t w, uint32_t h,
+                          size_t row_stride, const zr_view *views, size_t n_views, float lo,
+                          float hi, float *const *outputs);
+
+/* Device-resident variant over several frames already in HBM: view v samples frame
+ * view_frame[v].  `frames` is a host array whose rgba pointers are device pointers. */
+int zr_cnn_estimate_views_async(zr_session *s, const zr_frame *frames, size_t n_frames,
+                                const zr_view *views, const uint32_t *view_frame, size_t n_views,
+                                float lo, float hi, float *const *d_outputs, void *hip_stream);
+
+/* The preprocessing alone (K1), into `d_out` as [n_views,3,oh,ow] f32 (device). */
+int zr_preprocess_views_async(const zr_frame *frames, size_t n_frames, const zr_view *views,
+                              const uint32_t *view_frame, size_t n_views, uint32_t ow,
+                              uint32_t oh, float lo, float hi, float *d_out, void *hip_stream);
+
+/* Detector candidate compaction (device): per image, every anchor whose raw logit is
+ * >= logit_min is written as {anchor index bits, logit, params[0..D)} into d_rec
+ * ([n][cap][2+D]) and counted in d_count[n] (may exceed cap).  The exact sigmoid /
+ * threshold / decode / NMS then runs on the host (face/detection.rs:96-157, nms.rs:59-145). */
+int zr_detection_candidates_async(const float *d_logits, const float *d_boxes, uint32_t n,
+                                  uint32_t anchors, uint32_t params, float logit_min,
+                                  uint32_t cap, int32_t *d_count, float *d_rec, void *hip_stream);
+
+/* Roofline accounting of the compiled plan: algorithmic bytes and FLOPs per image, number
+ * of kernel launches per run. */
+int zr_session_stats(const zr_session *s, double *bytes_per_image, double *flops_per_image,
+                     size_t *launches);
+
+/* Compile a model without a GPU and describe the fused launch plan as text, one launch per
+ * line (for tests and diagnostics).  Writes at most `cap` bytes incl. the NUL terminator;
+ * `*needed` receives the full length + 1. */
+int zr_plan_describe(const uint8_t *onnx, size_t len, const uint32_t *out_sel, size_t n_sel,
+                     char *buf, size_t cap, size_t *needed);
+
+/* Thread-local text of the last error (anyhow::Error text). */
+const char *zr_last_error(void);
+
+/* Minimal device-memory helpers so host code needs no HIP headers. kind: 0 H2D, 1 D2H, 2 D2D */
+int zr_device_count(int *n);
+int zr_malloc(void **p, size_t bytes);
+int zr_free(void *p);
+int zr_memcpy_async(void *dst, const void *src, size_t bytes, int kind, void *hip_stream);
+int zr_stream_create(void **stream);
+int zr_stream_destroy(void *stream);
+int zr_stream_synchronize(void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZARU_HIP_H */

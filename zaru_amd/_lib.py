@@ -1,0 +1,144 @@
+"""ctypes binding of the C ABI in include/zaru_hip.h (zaru_amd/lib/libzaru_hip.so).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``make -C zaru_amd/csrc``).
+There is no fallback: if the shared object is missing or has no GPU to run on, every
+entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(HERE, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libzaru_hip.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "zaru_hip.h")
+
+ZR_OK = 0
+ERRORS = {-1: "invalid argument", -2: "model", -3: "device", -4: "shape"}
+
+
+class ZaruError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)} error: {msg}")
+        self.code = code
+
+
+class View(C.Structure):
+    """zr_view: RotatedRect in root-image coordinates (centre, size, clockwise radians)."""
+    _fields_ = [("cx", C.c_float), ("cy", C.c_float), ("w", C.c_float), ("h", C.c_float),
+                ("rad", C.c_float)]
+
+
+class Frame(C.Structure):
+    _fields_ = [("rgba", C.c_void_p), ("width", C.c_uint32), ("height", C.c_uint32),
+                ("row_stride", C.c_uint64)]
+
+
+_LIB = None
+
+# (name, restype, argtypes) for every exported entry point of include/zaru_hip.h
+_P, _SZ, _F, _U32, _I = C.c_void_p, C.c_size_t, C.c_float, C.c_uint32, C.c_int
+SIGNATURES = [
+    ("zr_session_create", _I, [_P, _SZ, _P, _SZ, _I, C.POINTER(_P)]),
+    ("zr_session_destroy", None, [_P]),
+    ("zr_session_num_io", _I, [_P, _I, C.POINTER(_SZ)]),
+    ("zr_session_io", _I, [_P, _I, _SZ, C.POINTER(C.c_char_p), _P, C.POINTER(_SZ)]),
+    ("zr_session_run", _I, [_P, _SZ, _P, _SZ, _P, _SZ]),
+    ("zr_session_run_async", _I, [_P, _SZ, _P, _P, _SZ, _P]),
+    ("zr_cnn_estimate_views", _I, [_P, _P, _U32, _U32, _SZ, _P, _SZ, _F, _F, _P]),
+    ("zr_cnn_estimate_views_async", _I, [_P, _P, _SZ, _P, _P, _SZ, _F, _F, _P, _P]),
+    ("zr_preprocess_views_async", _I, [_P, _SZ, _P, _P, _SZ, _U32, _U32, _F, _F, _P, _P]),
+    ("zr_detection_candidates_async", _I, [_P, _P, _U32, _U32, _U32, _F, _U32, _P, _P, _P]),
+    ("zr_session_stats", _I, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(_SZ)]),
+    ("zr_plan_describe", _I, [_P, _SZ, _P, _SZ, _P, _SZ, C.POINTER(_SZ)]),
+    ("zr_last_error", C.c_char_p, []),
+    ("zr_device_count", _I, [C.POINTER(_I)]),
+    ("zr_malloc", _I, [C.POINTER(_P), _SZ]),
+    ("zr_free", _I, [_P]),
+    ("zr_memcpy_async", _I, [_P, _P, _SZ, _I, _P]),
+    ("zr_stream_create", _I, [C.POINTER(_P)]),
+    ("zr_stream_destroy", _I, [_P]),
+    ("zr_stream_synchronize", _I, [_P]),
+]
+
+
+def lib():
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise ZaruError(-3, f"HIP extension not built: {LIB_PATH} missing "
+                            "(run __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = L
+    return L
+
+
+def check(rc: int):
+    if rc != ZR_OK:
+        raise ZaruError(rc, lib().zr_last_error().decode(errors="replace"))
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    check(lib().zr_device_count(C.byref(n)))
+    return n.value
+
+
+def plan_describe(onnx: bytes, outputs=None) -> str:
+    sel = (C.c_uint32 * len(outputs))(*outputs) if outputs else None
+    need = C.c_size_t(0)
+    check(lib().zr_plan_describe(onnx, len(onnx), sel, len(outputs or []), None, 0,
+                                 C.byref(need)))
+    buf = C.create_string_buffer(need.value)
+    check(lib().zr_plan_describe(onnx, len(onnx), sel, len(outputs or []), buf, need.value,
+                                 C.byref(need)))
+    return buf.value.decode()
+
+
+class DeviceBuffer:
+    """Owning device allocation (through the C ABI helpers, no HIP/torch import needed)."""
+
+    def __init__(self, nbytes: int):
+        p = C.c_void_p()
+        check(lib().zr_malloc(C.byref(p), max(4, int(nbytes))))
+        self.ptr = p.value
+        self.nbytes = int(nbytes)
+
+    @classmethod
+    def from_array(cls, a, stream=None):
+        import numpy as np
+        a = np.ascontiguousarray(a)
+        b = cls(a.nbytes)
+        b.upload(a, stream)
+        return b
+
+    def upload(self, a, stream=None):
+        import numpy as np
+        a = np.ascontiguousarray(a)
+        check(lib().zr_memcpy_async(self.ptr, a.ctypes.data, a.nbytes, 0, stream))
+        check(lib().zr_stream_synchronize(stream))
+
+    def download(self, shape, dtype, stream=None):
+        import numpy as np
+        out = np.empty(shape, dtype)
+        check(lib().zr_memcpy_async(out.ctypes.data, self.ptr, out.nbytes, 1, stream))
+        check(lib().zr_stream_synchronize(stream))
+        return out
+
+    def free(self):
+        if getattr(self, "ptr", None) and _LIB is not None:
+            _LIB.zr_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        self.free()
+
+
+def synchronize(stream=None):
+    check(lib().zr_stream_synchronize(stream))

@@ -1,0 +1,125 @@
+// gemm.hip -- 1x1 convolution / Gemm / full-plane convolution as an f32 MFMA GEMM with the
+// whole BlazeBlock tail fused into the epilogue (bias, activation, channel-padded and
+// optionally 2x2-max-pooled residual, second activation) and the graph-output layout
+// (Transpose/Reshape/Concat) folded into the store addressing.
+//
+// out[m][j] = post( pre( sum_k W[m][k] * X[k][j] + b[m] ) + R[m][j] ),  j = n*P + q.
+//
+// Tiling (gfx950, wave64): v_mfma_f32_32x32x2_f32 (exact f32, 64 FLOP/clk/SIMD, the same
+// rate as the f32 VALU).  A workgroup is 4 waves; each wave owns 32 columns and MT 32-row
+// tiles (MT*16 accumulator VGPRs).  Weights are staged through LDS in K-chunks of 32 rows
+// ([k][m] layout: a half-wave reads 32 consecutive floats, conflict-free); the activation
+// operand is read straight from HBM into the B fragment (lane l: X[k0 + l/32][j0 + l%32],
+// two fully coalesced 128-B rows per wave instruction), 16 loads per lane in flight.
+// Reference: the 1x1 Conv / Gemm nodes of the four ONNX graphs executed by ORT/tract at
+// crates/zaru/src/nn/mod.rs:483-533.
+#include "../runtime/zr_kernels.h"
+#include "act.h"
+
+namespace zr {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int KC = 32;  // K rows per LDS stage
+
+template <int MT, bool FULLPLANE>
+__global__ __launch_bounds__(256) void gemm_kernel(const GemmParams P) {
+    __shared__ float sW[KC][MT * 32];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int kh = lane >> 5, col = lane & 31;
+    const int m0 = blockIdx.y * (MT * 32);
+    const int j = (blockIdx.x * 4 + wave) * 32 + col;
+    const bool valid = j < P.ncols;
+    const int jj = valid ? j : 0;
+    const int n = jj / P.P, q = jj - n * P.P;
+    const float *xc = P.x + (int64_t)n * P.x_sN + q;
+
+    f32x16 acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+    for (int kc = 0; kc < P.Kpad; kc += KC) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < KC * MT * 32; i += 256) {
+            const int r = i / (MT * 32), c = i - r * (MT * 32);
+            const int kk = kc + r, mm = m0 + c;
+            sW[r][c] = (kk < P.Kpad && mm < P.Mpad) ? P.wt[(int64_t)kk * P.Mpad + mm] : 0.f;
+        }
+        // activation fragments for this chunk: load from a clamped (always valid) row and
+        // zero the padded rows with a select, so no load sits behind a branch.
+        float b[KC / 2];
+#pragma unroll
+        for (int s = 0; s < KC / 2; ++s) {
+            const int k = kc + 2 * s + kh;
+            const int kcl = k < P.K ? k : P.K - 1;
+            float v;
+            if constexpr (FULLPLANE) {
+                const int ci = kcl / P.KK, kq = kcl - ci * P.KK;
+                v = xc[(int64_t)ci * P.x_sC + (int64_t)kq * P.x_sK];
+            } else {
+                v = xc[(int64_t)kcl * P.x_sC];
+            }
+            b[s] = k < P.K ? v : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < KC / 2; ++s)
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(sW[2 * s + kh][t * 32 + col], b[s],
+                                                              acc[t], 0, 0, 0);
+    }
+
+    if (!valid) return;
+    // C/D map of 32x32 MFMA: column = lane%32, row = (r&3) + 8*(r>>2) + 4*(lane/32)
+    float *ob = P.out + (int64_t)n * P.o_sN + (int64_t)q * P.o_sP;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = m0 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+            if (m >= P.M) continue;
+            float v = apply_act(P.pre, acc[t][r] + P.bias[m], m);
+            if (P.res_mode != 0 && m < P.r_C) {
+                const float *rb = P.r + (int64_t)n * P.r_sN + (int64_t)m * P.r_sC;
+                float rv;
+                if (P.res_mode == 1) {
+                    rv = rb[q];
+                } else {
+                    const int y = q / P.out_W, x = q - y * P.out_W;
+                    const float *s0 = rb + (int64_t)(2 * y) * P.r_W + 2 * x;
+                    rv = fmaxf(fmaxf(s0[0], s0[1]), fmaxf(s0[P.r_W], s0[P.r_W + 1]));
+                }
+                v += rv;
+            }
+            ob[(int64_t)m * P.o_sC] = apply_act(P.post, v, m);
+        }
+}
+
+template <int MT>
+static void launch_mt(const GemmParams &p, dim3 grid, hipStream_t s) {
+    if (p.KK > 1)
+        hipLaunchKernelGGL((gemm_kernel<MT, true>), grid, dim3(256), 0, s, p);
+    else
+        hipLaunchKernelGGL((gemm_kernel<MT, false>), grid, dim3(256), 0, s, p);
+}
+
+void launch_gemm(const GemmParams &p, hipStream_t s) {
+    const int mtiles = p.Mpad / 32;
+    const int bx = (p.ncols + 127) / 128;
+    // Largest M tile (operand reuse) that still leaves >= 2 workgroups per CU of parallelism.
+    int mt = 4;
+    while (mt > 1 && (int64_t)bx * ((mtiles + mt - 1) / mt) < 512) --mt;
+    if (mt > mtiles) mt = mtiles;
+    dim3 grid(bx, (mtiles + mt - 1) / mt);
+    switch (mt) {
+    case 4: launch_mt<4>(p, grid, s); break;
+    case 3: launch_mt<3>(p, grid, s); break;
+    case 2: launch_mt<2>(p, grid, s); break;
+    default: launch_mt<1>(p, grid, s); break;
+    }
+}
+
+}  // namespace zr

@@ -1,0 +1,525 @@
+// session.cpp -- the C ABI of include/zaru_hip.h: sessions, execution contexts and the
+// view-sampling entry points.  This is the HIP `Session` variant that sits where
+// `Session::Ort` / `Session::Tract` sit in the reference (crates/zaru/src/nn/mod.rs:377-381).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../../include/zaru_hip.h"
+#include "onnx_model.h"
+#include "plan.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return set_err(ZR_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// One set of scratch buffers + a private stream.  Sessions keep a small pool so concurrent
+// callers never share a workspace; reuse across streams is ordered by `done`.
+struct Ctx {
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    float *arena = nullptr;
+    size_t arena_floats = 0;
+    float *input = nullptr;  // network input staging
+    size_t input_floats = 0;
+    uint8_t *image = nullptr;  // host-image upload (zr_cnn_estimate_views)
+    size_t image_bytes = 0;
+    zr::ViewDesc *views = nullptr;
+    zr::FrameDesc *frames = nullptr;
+    size_t views_cap = 0, frames_cap = 0;
+    std::vector<float *> outs;  // device outputs for the synchronous entry points
+    std::vector<size_t> outs_floats;
+
+    ~Ctx() {
+        if (stream) (void)hipStreamSynchronize(stream);
+        (void)hipFree(arena);
+        (void)hipFree(input);
+        (void)hipFree(image);
+        (void)hipFree(views);
+        (void)hipFree(frames);
+        for (auto p : outs) (void)hipFree(p);
+        if (done) (void)hipEventDestroy(done);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+template <typename T>
+int grow(T *&p, size_t &cap, size_t need) {
+    if (cap >= need) return ZR_OK;
+    if (p) {
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipFree(p));
+        p = nullptr;
+    }
+    size_t n = need + need / 4 + 64;
+    HIP_TRY(hipMalloc((void **)&p, n * sizeof(T)));
+    cap = n;
+    return ZR_OK;
+}
+
+// f32 quantities of a view exactly as the reference derives them (rect.rs:135-137,417-423;
+// matrix.rs:571-579 with glibc cosf/sinf evaluated here on the host).
+zr::ViewDesc make_view(const zr_view &v, uint32_t frame) {
+#pragma clang fp contract(off)
+    zr::ViewDesc d{};
+    d.half_w = v.w * 0.5f;
+    d.half_h = v.h * 0.5f;
+    d.tl_x = v.cx - v.w * 0.5f;
+    d.tl_y = v.cy - v.h * 0.5f;
+    d.view_w = v.w;
+    d.view_h = v.h;
+    d.cos_r = cosf(v.rad);
+    d.sin_r = sinf(v.rad);
+    d.frame = frame;
+    return d;
+}
+
+}  // namespace
+
+struct zr_session {
+    int device = 0;
+    zr::Plan plan;
+    float *weights = nullptr;
+    std::vector<std::unique_ptr<Ctx>> pool;
+    std::mutex pool_mu;
+    size_t next = 0;
+
+    Ctx *acquire() {
+        std::lock_guard<std::mutex> g(pool_mu);
+        // prefer an idle context; grow the pool up to 8 under contention
+        for (size_t i = 0; i < pool.size(); i++) {
+            Ctx *c = pool[(next + i) % pool.size()].get();
+            if (c->mu.try_lock()) {
+                next = (next + i + 1) % pool.size();
+                return c;
+            }
+        }
+        if (pool.size() < 8) {
+            auto c = std::make_unique<Ctx>();
+            (void)hipSetDevice(device);
+            if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess)
+                return nullptr;
+            c->mu.lock();
+            pool.push_back(std::move(c));
+            return pool.back().get();
+        }
+        Ctx *c = pool[next].get();
+        next = (next + 1) % pool.size();
+        c->mu.lock();
+        return c;
+    }
+
+    ~zr_session() {
+        pool.clear();
+        (void)hipFree(weights);
+    }
+};
+
+namespace {
+
+struct CtxLock {
+    Ctx *c;
+    explicit CtxLock(Ctx *x) : c(x) {}
+    ~CtxLock() {
+        if (c) c->mu.unlock();
+    }
+};
+
+// enqueue the plan on `stream` with a context's workspace
+int enqueue(zr_session *s, Ctx *c, int N, const float *input, int64_t in_sN, int64_t in_sC,
+            float *const *outs, hipStream_t stream) {
+    const size_t need = (size_t)s->plan.arena_per_image * (size_t)N;
+    if (int rc = grow(c->arena, c->arena_floats, need ? need : 1)) return rc;
+    HIP_TRY(hipStreamWaitEvent(stream, c->done, 0));
+    zr::Binding b;
+    b.N = N;
+    b.input = input;
+    b.in_sN = in_sN;
+    b.in_sC = in_sC;
+    b.outputs = outs;
+    b.arena = c->arena;
+    b.weights = s->weights;
+    zr::run_plan(s->plan, b, stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->done, stream));
+    return ZR_OK;
+}
+
+int check_session(const zr_session *s) {
+    if (!s) return set_err(ZR_ERR_INVALID_ARGUMENT, "null session");
+    return ZR_OK;
+}
+
+int sync_outputs(zr_session *s, Ctx *c, size_t batch) {
+    const auto &po = s->plan.outputs;
+    c->outs.resize(po.size(), nullptr);
+    c->outs_floats.resize(po.size(), 0);
+    for (size_t i = 0; i < po.size(); i++)
+        if (int rc = grow(c->outs[i], c->outs_floats[i], (size_t)po[i].per_image * batch)) return rc;
+    return ZR_OK;
+}
+
+int upload_views(Ctx *c, const zr_frame *frames, size_t nf, const zr_view *views,
+                 const uint32_t *view_frame, size_t nv, hipStream_t stream) {
+    if (int rc = grow(c->views, c->views_cap, nv ? nv : 1)) return rc;
+    if (int rc = grow(c->frames, c->frames_cap, nf ? nf : 1)) return rc;
+    std::vector<zr::ViewDesc> vd(nv);
+    for (size_t i = 0; i < nv; i++) {
+        const uint32_t f = view_frame ? view_frame[i] : 0;
+        if (f >= nf) return set_err(ZR_ERR_INVALID_ARGUMENT, "view_frame index out of range");
+        vd[i] = make_view(views[i], f);
+    }
+    std::vector<zr::FrameDesc> fd(nf);
+    for (size_t i = 0; i < nf; i++) {
+        fd[i].rgba = frames[i].rgba;
+        fd[i].w = frames[i].width;
+        fd[i].h = frames[i].height;
+        fd[i].stride = frames[i].row_stride;
+    }
+    // pageable sources: HIP stages them before returning, so the vectors may die here
+    HIP_TRY(hipMemcpyAsync(c->views, vd.data(), nv * sizeof(zr::ViewDesc), hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(c->frames, fd.data(), nf * sizeof(zr::FrameDesc), hipMemcpyHostToDevice, stream));
+    return ZR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *zr_last_error(void) { return g_err.c_str(); }
+
+int zr_session_create(const uint8_t *onnx, size_t len, const uint32_t *out_sel, size_t n_sel,
+                      int device, zr_session **out) {
+    if (!onnx || !out) return set_err(ZR_ERR_INVALID_ARGUMENT, "null model or out pointer");
+    *out = nullptr;
+    zr::OnnxModel m;
+    std::string err;
+    if (!zr::parse_onnx(onnx, len, m, err)) return set_err(ZR_ERR_MODEL, "ONNX parse error: " + err);
+    auto s = std::make_unique<zr_session>();
+    s->device = device;
+    std::vector<uint32_t> sel(out_sel, out_sel + n_sel);
+    if (!zr::compile_plan(m, sel, s->plan, err)) return set_err(ZR_ERR_MODEL, err);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return set_err(ZR_ERR_DEVICE, "no HIP device " + std::to_string(device));
+    HIP_TRY(hipSetDevice(device));
+    const size_t wb = s->plan.weights.size() * sizeof(float);
+    HIP_TRY(hipMalloc((void **)&s->weights, wb ? wb : 4));
+    HIP_TRY(hipMemcpy(s->weights, s->plan.weights.data(), wb, hipMemcpyHostToDevice));
+    *out = s.release();
+    return ZR_OK;
+}
+
+void zr_session_destroy(zr_session *s) { delete s; }
+
+int zr_session_num_io(const zr_session *s, int is_output, size_t *n) {
+    if (int rc = check_session(s)) return rc;
+    if (!n) return set_err(ZR_ERR_INVALID_ARGUMENT, "null n");
+    *n = is_output ? s->plan.outputs.size() : 1;
+    return ZR_OK;
+}
+
+int zr_session_io(const zr_session *s, int is_output, size_t idx, const char **name,
+                  int64_t *shape, size_t *rank) {
+    if (int rc = check_session(s)) return rc;
+    if (!is_output) {
+        if (idx != 0) return set_err(ZR_ERR_INVALID_ARGUMENT, "input index out of range");
+        if (name) *name = s->plan.input_name.c_str();
+        if (shape) {
+            shape[0] = 1;
+            shape[1] = s->plan.in_C;
+            shape[2] = s->plan.in_H;
+            shape[3] = s->plan.in_W;
+        }
+        if (rank) *rank = 4;
+        return ZR_OK;
+    }
+    if (idx >= s->plan.outputs.size()) return set_err(ZR_ERR_INVALID_ARGUMENT, "output index out of range");
+    const auto &o = s->plan.outputs[idx];
+    if (name) *name = o.name.c_str();
+    if (shape)
+        for (size_t i = 0; i < o.shape.size() && i < 8; i++) shape[i] = i == 0 ? 1 : o.shape[i];
+    if (rank) *rank = o.shape.size();
+    return ZR_OK;
+}
+
+int zr_plan_describe(const uint8_t *onnx, size_t len, const uint32_t *out_sel, size_t n_sel,
+                     char *buf, size_t cap, size_t *needed) {
+    if (!onnx) return set_err(ZR_ERR_INVALID_ARGUMENT, "null model");
+    zr::OnnxModel m;
+    std::string err;
+    if (!zr::parse_onnx(onnx, len, m, err)) return set_err(ZR_ERR_MODEL, "ONNX parse error: " + err);
+    zr::Plan plan;
+    std::vector<uint32_t> sel(out_sel, out_sel + n_sel);
+    if (!zr::compile_plan(m, sel, plan, err)) return set_err(ZR_ERR_MODEL, err);
+    static const char *kinds[] = {"gemm", "dw", "direct", "elt", "resize", "gap"};
+    static const char *acts[] = {"none", "relu", "clip", "prelu", "sigmoid"};
+    std::string t;
+    char line[512];
+    auto ref = [](const zr::TRef &r) {
+        char b[96];
+        snprintf(b, sizeof b, "%s%d[%dx%dx%d]", r.kind == 0 ? "t" : r.kind == 1 ? "in" : "out",
+                 r.id, r.C, r.H, r.W);
+        return std::string(b);
+    };
+    snprintf(line, sizeof line, "input %s %dx%dx%d arena_per_image=%lld weights=%zu bytes/img=%.0f flops/img=%.0f\n",
+             plan.input_name.c_str(), plan.in_C, plan.in_H, plan.in_W,
+             (long long)plan.arena_per_image, plan.weights.size(), plan.bytes_per_image,
+             plan.flops_per_image);
+    t += line;
+    for (auto &o : plan.outputs) {
+        snprintf(line, sizeof line, "output %s per_image=%lld\n", o.name.c_str(), (long long)o.per_image);
+        t += line;
+    }
+    for (auto &st : plan.steps) {
+        snprintf(line, sizeof line,
+                 "%s in=%s out=%s k=%dx%d s=%d M=%d K=%d KK=%d pre=%s post=%s res=%d rC=%d elt=%d off=%lld oN=%lld oC=%lld oP=%lld\n",
+                 kinds[st.kind], ref(st.in).c_str(), ref(st.out).c_str(), st.kh, st.kw, st.stride,
+                 st.M, st.K, st.KK, acts[st.pre.kind], acts[st.post.kind], st.res_mode, st.r_C,
+                 st.elt_op, (long long)st.out.off, (long long)st.out.o_sN, (long long)st.out.o_sC,
+                 (long long)st.out.o_sP);
+        t += line;
+    }
+    if (needed) *needed = t.size() + 1;
+    if (buf && cap) {
+        size_t n = std::min(cap - 1, t.size());
+        memcpy(buf, t.data(), n);
+        buf[n] = 0;
+    }
+    return ZR_OK;
+}
+
+int zr_session_stats(const zr_session *s, double *bytes, double *flops, size_t *launches) {
+    if (int rc = check_session(s)) return rc;
+    if (bytes) *bytes = s->plan.bytes_per_image;
+    if (flops) *flops = s->plan.flops_per_image;
+    if (launches) *launches = s->plan.steps.size();
+    return ZR_OK;
+}
+
+int zr_session_run_async(zr_session *s, size_t batch, const float *d_input, float *const *d_outputs,
+                         size_t n_out, void *hip_stream) {
+    if (int rc = check_session(s)) return rc;
+    if (!d_input || !d_outputs || batch == 0) return set_err(ZR_ERR_INVALID_ARGUMENT, "null tensor or empty batch");
+    if (n_out != s->plan.outputs.size()) return set_err(ZR_ERR_SHAPE, "output count mismatch");
+    Ctx *c = s->acquire();
+    if (!c) return set_err(ZR_ERR_DEVICE, "cannot create execution context");
+    CtxLock lk(c);
+    HIP_TRY(hipSetDevice(s->device));
+    const int64_t hw = (int64_t)s->plan.in_H * s->plan.in_W;
+    return enqueue(s, c, (int)batch, d_input, hw * s->plan.in_C, hw, d_outputs,
+                   (hipStream_t)hip_stream);
+}
+
+int zr_session_run(zr_session *s, size_t batch, const float *const *inputs, size_t n_in,
+                   float *const *outputs, size_t n_out) {
+    if (int rc = check_session(s)) return rc;
+    if (!inputs || !outputs || batch == 0) return set_err(ZR_ERR_INVALID_ARGUMENT, "null tensor or empty batch");
+    if (n_in != 1) return set_err(ZR_ERR_SHAPE, "CNN sessions take exactly 1 input");
+    if (n_out != s->plan.outputs.size()) return set_err(ZR_ERR_SHAPE, "output count mismatch");
+    Ctx *c = s->acquire();
+    if (!c) return set_err(ZR_ERR_DEVICE, "cannot create execution context");
+    CtxLock lk(c);
+    HIP_TRY(hipSetDevice(s->device));
+    const int64_t hw = (int64_t)s->plan.in_H * s->plan.in_W;
+    const size_t in_floats = (size_t)hw * s->plan.in_C * batch;
+    if (int rc = grow(c->input, c->input_floats, in_floats)) return rc;
+    if (int rc = sync_outputs(s, c, batch)) return rc;
+    HIP_TRY(hipMemcpyAsync(c->input, inputs[0], in_floats * 4, hipMemcpyHostToDevice, c->stream));
+    if (int rc = enqueue(s, c, (int)batch, c->input, hw * s->plan.in_C, hw, c->outs.data(), c->stream))
+        return rc;
+    for (size_t i = 0; i < n_out; i++)
+        HIP_TRY(hipMemcpyAsync(outputs[i], c->outs[i], s->plan.outputs[i].per_image * batch * 4,
+                               hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return ZR_OK;
+}
+
+static int views_common(zr_session *s, Ctx *c, const zr_frame *frames, size_t nf, const zr_view *views,
+                        const uint32_t *view_frame, size_t nv, float lo, float hi, float *const *outs,
+                        hipStream_t stream) {
+    const int64_t hw = (int64_t)s->plan.in_H * s->plan.in_W;
+    if (s->plan.in_C != 3) return set_err(ZR_ERR_SHAPE, "view sampling needs a 3-channel input");
+    if (!(hi > lo)) return set_err(ZR_ERR_INVALID_ARGUMENT, "ColorMapper range must satisfy end > start");
+    if (int rc = grow(c->input, c->input_floats, (size_t)hw * 3 * nv)) return rc;
+    HIP_TRY(hipStreamWaitEvent(stream, c->done, 0));
+    if (int rc = upload_views(c, frames, nf, views, view_frame, nv, stream)) return rc;
+    zr::PreprocParams p{};
+    p.frames = c->frames;
+    p.views = c->views;
+    p.nviews = (int)nv;
+    p.OW = s->plan.in_W;
+    p.OH = s->plan.in_H;
+    p.lo = lo;
+    p.adjust = (hi - lo) / 255.0f;  // nn/mod.rs:162
+    p.out = c->input;
+    p.o_sN = hw;                    // CNHW straight into the plan's input layout
+    p.o_sC = hw * (int64_t)nv;
+    zr::launch_preproc(p, stream);
+    HIP_TRY(hipGetLastError());
+    return enqueue(s, c, (int)nv, c->input, hw, hw * (int64_t)nv, outs, stream);
+}
+
+int zr_cnn_estimate_views_async(zr_session *s, const zr_frame *frames, size_t n_frames,
+                                const zr_view *views, const uint32_t *view_frame, size_t n_views,
+                                float lo, float hi, float *const *d_outputs, void *hip_stream) {
+    if (int rc = check_session(s)) return rc;
+    if (!frames || !views || !d_outputs || n_views == 0)
+        return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument or no views");
+    Ctx *c = s->acquire();
+    if (!c) return set_err(ZR_ERR_DEVICE, "cannot create execution context");
+    CtxLock lk(c);
+    HIP_TRY(hipSetDevice(s->device));
+    return views_common(s, c, frames, n_frames, views, view_frame, n_views, lo, hi, d_outputs,
+                        (hipStream_t)hip_stream);
+}
+
+int zr_cnn_estimate_views(zr_session *s, const uint8_t *rgba, uint32_t w, uint32_t h,
+                          size_t row_stride, const zr_view *views, size_t n_views, float lo,
+                          float hi, float *const *outputs) {
+    if (int rc = check_session(s)) return rc;
+    if (!rgba || !views || !outputs || n_views == 0)
+        return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument or no views");
+    if (row_stride < (size_t)w * 4) return set_err(ZR_ERR_INVALID_ARGUMENT, "row_stride < 4*width");
+    Ctx *c = s->acquire();
+    if (!c) return set_err(ZR_ERR_DEVICE, "cannot create execution context");
+    CtxLock lk(c);
+    HIP_TRY(hipSetDevice(s->device));
+    const size_t bytes = row_stride * h;
+    if (int rc = grow(c->image, c->image_bytes, bytes ? bytes : 4)) return rc;
+    if (int rc = sync_outputs(s, c, n_views)) return rc;
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->done, 0));
+    HIP_TRY(hipMemcpyAsync(c->image, rgba, bytes, hipMemcpyHostToDevice, c->stream));
+    zr_frame f{c->image, w, h, (uint64_t)row_stride};
+    if (int rc = views_common(s, c, &f, 1, views, nullptr, n_views, lo, hi, c->outs.data(), c->stream))
+        return rc;
+    for (size_t i = 0; i < s->plan.outputs.size(); i++)
+        HIP_TRY(hipMemcpyAsync(outputs[i], c->outs[i], s->plan.outputs[i].per_image * n_views * 4,
+                               hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return ZR_OK;
+}
+
+int zr_preprocess_views_async(const zr_frame *frames, size_t n_frames, const zr_view *views,
+                              const uint32_t *view_frame, size_t n_views, uint32_t ow, uint32_t oh,
+                              float lo, float hi, float *d_out, void *hip_stream) {
+    if (!frames || !views || !d_out || n_views == 0 || ow == 0 || oh == 0)
+        return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument or empty shape");
+    if (!(hi > lo)) return set_err(ZR_ERR_INVALID_ARGUMENT, "ColorMapper range must satisfy end > start");
+    hipStream_t st = (hipStream_t)hip_stream;
+    std::vector<zr::ViewDesc> vd(n_views);
+    for (size_t i = 0; i < n_views; i++) {
+        const uint32_t f = view_frame ? view_frame[i] : 0;
+        if (f >= n_frames) return set_err(ZR_ERR_INVALID_ARGUMENT, "view_frame index out of range");
+        vd[i] = make_view(views[i], f);
+    }
+    std::vector<zr::FrameDesc> fd(n_frames);
+    for (size_t i = 0; i < n_frames; i++)
+        fd[i] = zr::FrameDesc{frames[i].rgba, frames[i].width, frames[i].height, frames[i].row_stride};
+    zr::ViewDesc *dv = nullptr;
+    zr::FrameDesc *df = nullptr;
+    HIP_TRY(hipMallocAsync((void **)&dv, n_views * sizeof(zr::ViewDesc), st));
+    HIP_TRY(hipMallocAsync((void **)&df, n_frames * sizeof(zr::FrameDesc), st));
+    HIP_TRY(hipMemcpyAsync(dv, vd.data(), n_views * sizeof(zr::ViewDesc), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(df, fd.data(), n_frames * sizeof(zr::FrameDesc), hipMemcpyHostToDevice, st));
+    zr::PreprocParams p{};
+    p.frames = df;
+    p.views = dv;
+    p.nviews = (int)n_views;
+    p.OW = (int)ow;
+    p.OH = (int)oh;
+    p.lo = lo;
+    p.adjust = (hi - lo) / 255.0f;
+    p.out = d_out;
+    p.o_sN = 3 * (int64_t)ow * oh;
+    p.o_sC = (int64_t)ow * oh;
+    zr::launch_preproc(p, st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipFreeAsync(dv, st));
+    HIP_TRY(hipFreeAsync(df, st));
+    return ZR_OK;
+}
+
+int zr_detection_candidates_async(const float *d_logits, const float *d_boxes, uint32_t n,
+                                  uint32_t anchors, uint32_t params, float logit_min,
+                                  uint32_t cap, int32_t *d_count, float *d_rec, void *hip_stream) {
+    if (!d_logits || !d_boxes || !d_count || !d_rec) return set_err(ZR_ERR_INVALID_ARGUMENT, "null pointer");
+    if (n == 0) return ZR_OK;
+    zr::CandParams p{};
+    p.logits = d_logits;
+    p.boxes = d_boxes;
+    p.N = (int)n;
+    p.A = (int)anchors;
+    p.D = (int)params;
+    p.cap = (int)cap;
+    p.logit_min = logit_min;
+    p.count = d_count;
+    p.rec = d_rec;
+    zr::launch_candidates(p, (hipStream_t)hip_stream);
+    HIP_TRY(hipGetLastError());
+    return ZR_OK;
+}
+
+int zr_device_count(int *n) {
+    if (!n) return set_err(ZR_ERR_INVALID_ARGUMENT, "null n");
+    *n = 0;
+    if (hipGetDeviceCount(n) != hipSuccess) *n = 0;
+    return ZR_OK;
+}
+
+int zr_malloc(void **p, size_t bytes) {
+    if (!p) return set_err(ZR_ERR_INVALID_ARGUMENT, "null p");
+    HIP_TRY(hipMalloc(p, bytes ? bytes : 4));
+    return ZR_OK;
+}
+
+int zr_free(void *p) {
+    HIP_TRY(hipFree(p));
+    return ZR_OK;
+}
+
+int zr_memcpy_async(void *dst, const void *src, size_t bytes, int kind, void *hip_stream) {
+    hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost
+                                                                    : hipMemcpyDeviceToDevice;
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, k, (hipStream_t)hip_stream));
+    return ZR_OK;
+}
+
+int zr_stream_create(void **stream) {
+    if (!stream) return set_err(ZR_ERR_INVALID_ARGUMENT, "null stream");
+    HIP_TRY(hipStreamCreateWithFlags((hipStream_t *)stream, hipStreamNonBlocking));
+    return ZR_OK;
+}
+
+int zr_stream_destroy(void *stream) {
+    HIP_TRY(hipStreamDestroy((hipStream_t)stream));
+    return ZR_OK;
+}
+
+int zr_stream_synchronize(void *stream) {
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    return ZR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,156 @@
+// zr_kernels.h -- launch descriptors shared by the graph runtime and the gfx950 kernels.
+//
+// Activation layout in HBM ("CNHW"): element (n, c, p) of an internal tensor with
+// N images, C channels and P = H*W positions lives at  c*(N*P) + n*P + p.  Every
+// 1x1 convolution is then a plain GEMM  out[Cout][N*P] = W[Cout][Cin] . X[Cin][N*P]
+// with both operands contiguous along the column axis, whatever the spatial size.
+// Graph outputs are written directly in the reference's row-major layout (batch in
+// dim 0) through explicit (sN, sC, sP) strides, so no transpose/reshape/concat ever
+// runs as a separate pass.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace zr {
+
+enum ActKind : int { ACT_NONE = 0, ACT_RELU = 1, ACT_CLIP = 2, ACT_PRELU = 3, ACT_SIGMOID = 4 };
+
+struct Act {
+    int kind = ACT_NONE;
+    float lo = 0.f, hi = 0.f;        // Clip bounds
+    const float *slope = nullptr;    // PReLU per-channel slope (device)
+};
+
+// Generic strided view of a 4-D activation: element (n, c, y, x) at
+// base + n*sN + c*sC + y*sY + x  (x is always unit stride).
+struct Plane {
+    const float *p;
+    int64_t sN, sC;
+    int C, H, W;
+};
+
+// ---------------------------------------------------------------- GEMM (1x1 conv / Gemm /
+// full-plane conv).  Column j = n*P + q  (P output positions per image).
+// B operand X(k, j): x + n*x_sN + (k / KK)*x_sC + (k % KK)*x_sK + q   (KK = 1 except for a
+// convolution whose kernel covers its whole input plane, where KK = kh*kw and P = 1).
+struct GemmParams {
+    const float *x;
+    int64_t x_sN, x_sC;
+    int KK, x_sK;
+    int P, ncols;        // positions per image, N*P
+    int M, K;            // Cout, reduction length (Cin*KK)
+    int Mpad, Kpad;      // weights zero-padded to multiples of 32 / 8
+    const float *wt;     // [Kpad][Mpad]  (transposed)
+    const float *bias;   // [Mpad]
+    Act pre, post;       // y = post( pre(acc + bias) + residual )
+    // residual (channel-padded, optionally 2x2 max-pooled) source
+    int res_mode;        // 0 none, 1 direct, 2 maxpool 2x2/2
+    const float *r;
+    int64_t r_sN, r_sC;
+    int r_C, r_W;        // channels present in the residual (rest are zero); source width
+    int out_W;           // output width (to split q into y, x for pooling)
+    // output (m, j) at out + n*o_sN + m*o_sC + q*o_sP
+    float *out;
+    int64_t o_sN, o_sC, o_sP;
+};
+
+// ---------------------------------------------------------------- depthwise conv
+struct DwParams {
+    Plane in;
+    float *out;
+    int64_t o_sN, o_sC;
+    int OH, OW, N;
+    int k, stride, pad_t, pad_l;
+    const float *w;      // [C][k*k]
+    const float *bias;   // [C]
+    Act act;
+};
+
+// ---------------------------------------------------------------- dense direct conv
+struct DirectParams {
+    Plane in;
+    float *out;
+    int64_t o_sN, o_sC;
+    int OH, OW, N, Cout;
+    int kh, kw, stride, pad_t, pad_l;
+    const float *w;      // [Cout][Cin][kh][kw]
+    const float *bias;   // [Cout]
+    Act act;
+};
+
+// ---------------------------------------------------------------- elementwise family
+struct EltParams {
+    int op;              // 0 act-copy, 1 add(a,b), 2 maxpool2 of a, 3 channel-pad of a
+    Plane a, b;          // sources (b only for add)
+    float *out;
+    int64_t o_sN, o_sC;
+    int N, C, H, W;      // output geometry
+    Act act;
+};
+
+struct ResizeParams {    // bilinear, half_pixel, edge clamp
+    Plane in;
+    float *out;
+    int64_t o_sN, o_sC;
+    int N, OH, OW;
+    float scale_y, scale_x;  // in/out ratio
+};
+
+struct GapParams {
+    Plane in;
+    float *out;
+    int64_t o_sN, o_sC;
+    int N;
+};
+
+// ---------------------------------------------------------------- preprocessing
+// One view: a RotatedRect in root-image coordinates (image/mod.rs:188-192) with its
+// host-computed (glibc) cos/sin and the derived f32 quantities the reference recomputes
+// per sample.  All arithmetic in the kernel is IEEE f32 without contraction.
+struct ViewDesc {
+    float half_w, half_h;    // rect.size() * 0.5
+    float tl_x, tl_y;        // rect.top_left() = centre - size * 0.5
+    float view_w, view_h;    // rect.size()
+    float cos_r, sin_r;      // cosf(rad), sinf(rad)
+    uint32_t frame;          // index into the frame array
+    uint32_t pad_;
+};
+
+struct FrameDesc {
+    const uint8_t *rgba;
+    uint32_t w, h;
+    uint64_t stride;         // bytes per row
+};
+
+struct PreprocParams {
+    const FrameDesc *frames;
+    const ViewDesc *views;
+    int nviews, OW, OH;
+    float lo, adjust;        // ColorMapper: c * adjust + lo
+    float *out;              // (view v, channel c, position q) at out + v*o_sN + c*o_sC + q
+    int64_t o_sN, o_sC;
+};
+
+// ---------------------------------------------------------------- detection candidates
+// Per image: anchors whose logit >= logit_min (a conservative bound below logit(thresh))
+// are compacted as {anchor index, logit, raw box params} for the exact host decode.
+struct CandParams {
+    const float *logits;     // [N][A]
+    const float *boxes;      // [N][A][D]
+    int N, A, D, cap;
+    float logit_min;
+    int *count;              // [N]
+    float *rec;              // [N][cap][2 + D]
+};
+
+// launchers (kernels/*.hip)
+void launch_gemm(const GemmParams &p, hipStream_t s);
+void launch_dw(const DwParams &p, hipStream_t s);
+void launch_direct(const DirectParams &p, hipStream_t s);
+void launch_elt(const EltParams &p, hipStream_t s);
+void launch_resize(const ResizeParams &p, hipStream_t s);
+void launch_gap(const GapParams &p, hipStream_t s);
+void launch_preproc(const PreprocParams &p, hipStream_t s);
+void launch_candidates(const CandParams &p, hipStream_t s);
+
+}  // namespace zr
