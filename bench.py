@@ -1,0 +1,290 @@
+#!/usr/bin/env python3
+"""Benchmark: end-to-end faces/sec (BlazeFace detect + 468-pt FaceMesh) on synthetic 1080p
+frames, one process per GPU (BASELINE.json metric, config 3; config 5's frame sharding for
+N > 1).
+
+A step = one batch of `--batch` 1920x1080 RGBA8 frames per GPU, already resident in HBM,
+through the whole reference call chain (crates/zaru/src/detection.rs:216-270 then one
+LandmarkTracker pass per face, landmark.rs:463-501): GPU letterbox preprocessing + BlazeFace,
+exact host decode + weighted NMS, GPU ROI preprocessing + FaceMesh, host landmark mapping and
+ROI update.  With N > 1 every rank all-gathers its fixed-size detection records over RCCL
+(the single collective of SURVEY.md §8e) inside the timed region.
+
+Synthetic data: seeded uniform-noise frames carrying one synthetic face patch per frame
+(tools/make_face_patch.py) when available; frames whose detector finds nothing are tracked on a
+seeded square ROI ("forced-ROI mode") so every frame runs FaceMesh once.
+
+Prints ONE JSON line (rank 0).  `--workload hand` runs config 4 (palm + 4 hand ROIs) instead.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md chip table)
+FP32_PEAK_TFLOPS = 157.3   # f32 MFMA = f32 VALU peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="frames per step per GPU")
+    ap.add_argument("--workload", choices=["face", "hand"], default="face")
+    ap.add_argument("--threads", type=int, default=16, help="host decode/map threads per rank")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    return ap.parse_args()
+
+
+def make_frames(rng, n, h=1080, w=1920, patch=None):
+    frames = rng.integers(0, 256, size=(n, h, w, 4), dtype=np.uint8)
+    centers = []
+    for i in range(n):
+        if patch is not None:
+            ph, pw = patch.shape[:2]
+            y = int(rng.integers(0, h - ph))
+            x = int(rng.integers(0, w - pw))
+            frames[i, y:y + ph, x:x + pw] = patch
+            centers.append((x + pw / 2, y + ph / 2, pw))
+        else:
+            centers.append(None)
+    return frames, centers
+
+
+def forced_rois(rng, n, workload, h=1080, w=1920):
+    out = []
+    for _ in range(n):
+        k = 1 if workload == "face" else 4
+        rois = []
+        for _ in range(k):
+            side = float(rng.uniform(150, 400))
+            cx = float(rng.uniform(side / 2, w - side / 2))
+            cy = float(rng.uniform(side / 2, h - side / 2))
+            rad = 0.0 if workload == "face" else float(rng.uniform(-math.pi, math.pi))
+            rois.append((cx, cy, side, side, rad))
+        out.append(rois)
+    return out
+
+
+def load_patch():
+    p = os.path.join(REPO, "tests", "golden", "face_patch.npy")
+    return np.load(p) if os.path.exists(p) else None
+
+
+# ---------------------------------------------------------------- CPU baseline (oracle)
+def cpu_baseline(frames, forced, workload, budget_s):
+    """The reference path restated on the host (oracle/, single thread): same frames, same
+    stages.  Label: reference-semantics C restatement, ORT/tract unavailable."""
+    import oracle as O
+    models = os.path.join(REPO, "zaru_amd", "models")
+    if workload == "face":
+        det = O.Net(os.path.join(models, "face_detection_short_range.onnx"), f64=False)
+        lm = O.Net(os.path.join(models, "face_landmark.onnx"), f64=False)
+        din, lin, dlo, llo, kind = 128, 192, -1.0, -1.0, O.FACE
+    else:
+        det = O.Net(os.path.join(models, "palm_detection_lite.onnx"), f64=False)
+        lm = O.Net(os.path.join(models, "hand_landmark_lite.onnx"), f64=False)
+        din, lin, dlo, llo, kind = 192, 224, 0.0, 0.0, O.PALM
+    t0 = time.perf_counter()
+    nframes = nfaces = 0
+    for i in range(len(frames)):
+        img = frames[i]
+        h, w = img.shape[:2]
+        r = O.grow_to_fit_aspect(O.Rect.from_top_left(0, 0, w, h), din, din)
+        v = O.view_compose(O.view_full(w, h), r)
+        x = O.preproc(img, v, din, din, dlo, 1.0)
+        reg, cls = det.run(x[None])
+        dets = O.detect_post(kind, reg[0], cls[0], w, h, din, din)
+        if dets:
+            grow = 0.0 if workload == "face" else 1.5
+            rois = [O.RRect(O.grow_rel(d.rect, grow) if grow else d.rect,
+                            d.angle if workload == "hand" else 0.0) for d in dets]
+        else:
+            rois = [O.RRect(O.Rect(*f[:4]), f[4]) for f in forced[i]]
+        for roi in rois:
+            vr = O.RRect(O.grow_to_fit_aspect(roi.rect, 1, 1), roi.rad)
+            view = O.view_compose(O.view_full(w, h), vr)
+            lrect = O.grow_to_fit_aspect(O.Rect.from_top_left(0, 0, view.rect.w, view.rect.h), 1, 1)
+            v2 = O.view_compose(view, lrect)
+            xl = O.preproc(img, v2, lin, lin, llo, 1.0)
+            outs = lm.run(xl[None])
+            pos = O.estimator_map(outs[0].reshape(-1, 3), lrect, lin)
+            O.tracker_update(pos, vr, roi.rad, 0.0, 0.3)
+            nfaces += 1
+        nframes += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": nfaces / dt, "unit": "faces/s" if workload == "face" else "hands/s",
+            "cores": 1, "kind": "port",
+            "sample": f"{nframes} synthetic 1080p frames / {nfaces} ROIs through oracle/ "
+                      f"(C restatement, f32, naive ONNX interpreter, 1 thread) in {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    device = local if world > 1 else 0
+    torch.cuda.set_device(device)
+
+    import zaru_amd.host as H
+
+    B = args.batch
+    rng = np.random.default_rng(3 + 1000 * rank)
+    patch = load_patch() if args.workload == "face" else None
+    frames_np, _ = make_frames(rng, B, patch=patch)
+    forced = forced_rois(rng, B, args.workload)
+    frames_t = torch.from_numpy(frames_np).to(f"cuda:{device}")
+    torch.cuda.synchronize()
+    fp = frames_t.data_ptr()
+    fbytes = 1080 * 1920 * 4
+    flist = [(fp + i * fbytes, 1920, 1080, 1920 * 4) for i in range(B)]
+
+    pipe = H.DetectTrackPipeline(args.workload, device, args.threads,
+                                 1 if args.workload == "face" else 4)
+    rec_w = 1 + 8 * 20
+    gather_in = torch.zeros((B, rec_w), dtype=torch.float32, device=f"cuda:{device}")
+    gather_out = torch.zeros((world * B, rec_w), dtype=torch.float32, device=f"cuda:{device}")
+
+    def step():
+        pipe.run(flist, forced)
+        if world > 1:
+            # one RCCL all-gather of fixed-size detection records per step
+            recs = np.zeros((B, rec_w), np.float32)
+            for f, dets in enumerate(pipe.detections()):
+                recs[f, 0] = len(dets)
+                for k, d in enumerate(dets[:8]):
+                    r = d.bounding_rect().tuple()
+                    recs[f, 1 + 20 * k:1 + 20 * k + 6] = (d.confidence(), d.angle(), *r)
+            gather_in.copy_(torch.from_numpy(recs))
+            dist.all_gather_into_tensor(gather_out, gather_in)
+        return pipe.num_rois()
+
+    for _ in range(args.warmup):
+        step()
+    if not args.no_profile:
+        pipe.profile_read()  # drop warmup records
+        pipe.profile(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    faces = 0
+    stage = {"detect_gpu_ms": 0.0, "decode_nms_ms": 0.0, "landmark_gpu_ms": 0.0, "map_ms": 0.0}
+    dets_total = 0
+    for _ in range(args.steps):
+        faces += step()
+        t = pipe.times()
+        for k in stage:
+            stage[k] += t[k]
+        dets_total += t["detections"]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = pipe.profile_read() if not args.no_profile else ""
+    pipe.profile(False)
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([faces], dtype=torch.float64, device=f"cuda:{device}")
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        faces_all = int(c.item())
+    else:
+        faces_all = faces
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    # ---- roofline of the dominant kernel, from the HIP-event records of the timed region
+    kernels = []
+    for line in prof.splitlines():
+        name, n, ms, by, fl = line.rsplit(" ", 4)
+        kernels.append({"kernel": name, "launches": int(n), "ms": float(ms), "bytes": float(by),
+                        "flops": float(fl)})
+    roofline = None
+    if kernels:
+        dom = max(kernels, key=lambda k: k["ms"])
+        avg_s = dom["ms"] / dom["launches"] / 1e3
+        gbs = dom["bytes"] / dom["launches"] / avg_s / 1e9
+        tfl = dom["flops"] / dom["launches"] / avg_s / 1e12
+        if tfl / FP32_PEAK_TFLOPS > gbs / HBM_PEAK_GBS:
+            roofline = {"bound": "mfma", "achieved": round(tfl, 3), "peak": FP32_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(tfl / FP32_PEAK_TFLOPS, 4)}
+        else:
+            roofline = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        roofline["traffic"] = None
+        roofline["kernel"] = dom["kernel"]
+        roofline["avg_launch_us"] = round(avg_s * 1e6, 2)
+        roofline["algorithmic_bytes_per_launch"] = round(dom["bytes"] / dom["launches"])
+        total_ms = sum(k["ms"] for k in kernels)
+        roofline["kernel_share"] = round(dom["ms"] / total_ms, 3)
+    st = pipe.stats()
+    frames_per_s = world * B * args.steps / elapsed
+    bytes_frame = st["detector_bytes_per_image"] + st["landmarker_bytes_per_image"] * faces / (B * args.steps)
+    pipeline_gbs_per_gpu = frames_per_s / world * bytes_frame / 1e9
+
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(frames_np, forced, args.workload, args.cpu_baseline_seconds)
+
+    unit = "faces/s" if args.workload == "face" else "hands/s"
+    out = {
+        "metric": "end-to-end faces/sec (detect+468-pt mesh), 1080p synthetic, 1/2/4/8 GPU"
+        if args.workload == "face" else "end-to-end hands/sec (palm detect + 21-pt hand landmarks, 4 ROIs/frame)",
+        "value": round(faces_all / elapsed, 1),
+        "unit": unit,
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: seeded uniform-noise 1920x1080 RGBA8 frames"
+                + (" + one synthetic face patch each" if load_patch() is not None and args.workload == "face" else "")
+                + "; forced seeded ROI when no detection; ONNX weights from the reference",
+        "config": {"workload": "face pipeline BlazeFace->FaceMesh V1 (config 3/5)" if args.workload == "face"
+                   else "palm lite + hand landmark lite, 4 ROIs/frame (config 4)",
+                   "frames_per_gpu_per_step": B, "frame": "1920x1080 RGBA8",
+                   "parallelism": f"frame-sharded x{world}" + (", RCCL all-gather of detections" if world > 1 else "")},
+        "frames_per_s": round(frames_per_s, 1),
+        "detections_per_step": round(dets_total / args.steps, 1),
+        "stage_ms_per_step": {k: round(v / args.steps, 3) for k, v in stage.items()},
+        "pipeline_algorithmic_GBs_per_gpu": round(pipeline_gbs_per_gpu, 1),
+        "roofline": roofline,
+        "kernels": sorted(kernels, key=lambda k: -k["ms"])[:8],
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -107,6 +107,13 @@ int zr_detection_candidates_async(const float *d_logits, const float *d_boxes, u
 int zr_session_stats(const zr_session *s, double *bytes_per_image, double *flops_per_image,
                      size_t *launches);
 
+/* Per-launch profiling with HIP events recorded on the launching stream around every kernel
+ * of this session (preprocessing included).  zr_profile_read returns and clears the
+ * aggregate, one line per kernel symbol: "<kernel> <launches> <total_ms> <bytes> <flops>"
+ * where bytes/flops are the algorithmic traffic/work of those launches. */
+int zr_profile_enable(zr_session *s, int enable);
+int zr_profile_read(zr_session *s, char *buf, size_t cap, size_t *needed);
+
 /* Compile a model without a GPU and describe the fused launch plan as text, one launch per
  * line (for tests and diagnostics).  Writes at most `cap` bytes incl. the NUL terminator;
  * `*needed` receives the full length + 1. */

@@ -1,0 +1,123 @@
+"""The C++ host layer (zaru_amd.host) against the reference's known-answer tests and the
+decode fixtures -- CPU only (no network inference involved)."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+import zaru_amd.host as H
+
+
+def f32(v):
+    return float(np.float32(v))
+
+
+def test_nms_kat(kat):
+    for c in kat["nms"]:
+        nms = H.NonMaxSuppression()
+        nms.set_mode(H.SuppressionMode.Remove if c["mode"] == "remove" else H.SuppressionMode.Average)
+        nms.set_iou_thresh(c["iou"])
+        dets = [H.Detection(conf, H.Rect.from_center(*r)) for conf, r in c["dets"]]
+        out = nms.process(dets)
+        if "want_len" in c:
+            assert len(out) == c["want_len"]
+            continue
+        assert len(out) == len(c["want"])
+        for d, (conf, r) in zip(out, c["want"]):
+            assert d.confidence() == f32(conf)
+            assert d.bounding_rect().tuple() == tuple(f32(v) for v in r)
+
+
+def test_rect_kat(kat):
+    for c in kat["iou"]:
+        assert H.Rect.from_center(*c["a"]).iou(H.Rect.from_center(*c["b"])) == c["want"]
+    for c in kat["intersection"]:
+        a, b = H.Rect.from_top_left(*c["a_tl"]), H.Rect.from_top_left(*c["b_tl"])
+        if "want_area" in c:
+            assert a.intersection_area(b) == c["want_area"]
+        else:
+            assert a.intersection(b) == H.Rect.from_top_left(*c["want_tl"])
+    for c in kat["fit_aspect"]:
+        r = H.Rect.from_center(*c["r"]).grow_to_fit_aspect(*c["aspect"])
+        assert r == H.Rect.from_center(*c["want"])
+    for c in kat["transform"]:
+        rr = H.RotatedRect(H.Rect.from_top_left(*c["tl"]), c["rad"])
+        got = (rr.transform_in if c["dir"] == "in" else rr.transform_out)(*c["p"])
+        if c.get("tol"):
+            assert all(abs(g - w) <= 1e-6 for g, w in zip(got, c["want"]))
+        else:
+            assert got == tuple(float(v) for v in c["want"])
+    for c in kat["rrect_bounding"]:
+        rr = H.RotatedRect.bounding(c["rad"], [tuple(p) for p in c["pts"]])
+        want = H.Rect.from_top_left(*c["want_tl"])
+        if c["exact"]:
+            assert rr.rect() == want and rr.rotation_radians() == f32(c["rad"])
+        else:
+            assert np.allclose(rr.rect().tuple(), want.tuple(), atol=1e-6)
+
+
+def test_view_data_kat(kat):
+    for c in kat["view_data"]:
+        v = H.ViewData.full(*c["image"])
+        for tl in c["chain"]:
+            v = v.view_rect(H.Rect.from_top_left(*tl))
+        assert v.rect.rect() == H.Rect.from_top_left(*c["want_tl"])
+
+
+def test_host_geometry_matches_oracle_randomized():
+    import oracle as O
+    rng = np.random.default_rng(3)
+    for _ in range(2000):
+        r = [float(np.float32(v)) for v in rng.uniform(-500, 500, 2)] + \
+            [float(np.float32(v)) for v in rng.uniform(0.1, 800, 2)]
+        rad = float(np.float32(rng.uniform(-7, 7)))
+        p = [float(np.float32(v)) for v in rng.uniform(-900, 900, 2)]
+        hr = H.RotatedRect(H.Rect.from_center(*r), rad)
+        orr = O.RRect(O.Rect(*r), rad)
+        assert hr.transform_out(*p) == O.transform_out(orr, *p)
+        assert hr.transform_in(*p) == O.transform_in(orr, *p)
+        a = H.Rect.from_center(*r)
+        b = H.Rect.from_center(*[float(np.float32(v)) for v in
+                                 (r[0] + rng.normal(0, 50), r[1] + rng.normal(0, 50), r[2] * 1.3, r[3])])
+        assert a.iou(b) == O.iou(O.Rect(*a.tuple()), O.Rect(*b.tuple())) or math.isnan(a.iou(b))
+        pv = H.ViewData.full(1920, 1080).view(hr)
+        ov = O.view_compose(O.view_full(1920, 1080), orr)
+        assert pv.rect.rect().tuple() == ov.rect.tuple() and pv.rect.rotation_radians() == ov.rad
+
+
+def test_decode_nms_bit_exact(golden_dir):
+    """Detector extract + NMS + map (detection.rs:231-267) bit-exact on fixture F3."""
+    g = np.load(os.path.join(golden_dir, "decode_cases.npz"))
+    keys = sorted({k.split("/")[0] for k in g.files})
+    for key in keys:
+        net = "palm" if key.startswith("palm") else "face"
+        iw, ih = (int(v) for v in g[f"{key}/img"])
+        dets = H.detect_post(net, g[f"{key}/boxes"], g[f"{key}/confs"], iw, ih)
+        want = g[f"{key}/want"]
+        assert len(dets) == len(want), key
+        for d, w in zip(dets, want):
+            rec = np.zeros_like(w)
+            rec[0], rec[1] = d.confidence(), d.angle()
+            rec[2:6] = d.bounding_rect().tuple()
+            for k, (x, y) in enumerate(d.keypoints()):
+                rec[6 + 2 * k], rec[7 + 2 * k] = x, y
+            assert np.array_equal(rec.view(np.uint32), w.view(np.uint32)), key
+
+
+def test_anchors_match_oracle():
+    import oracle as O
+    assert np.array_equal(H.anchors("face"), O.anchors(O.FACE_LAYERS))
+    assert np.array_equal(H.anchors("palm"), O.anchors(O.PALM_LAYERS))
+    assert H.anchors("face").shape == (896, 2) and H.anchors("palm").shape == (2016, 2)
+
+
+def test_candidate_floor_is_conservative():
+    """Device compaction keeps every anchor the exact host test could keep."""
+    import oracle as O
+    for t in (0.5, 0.3, 0.75, 0.9, 0.05):
+        lf = H.candidate_logit_floor(t)
+        # every logit below the floor must fail the reference's f32 test sigmoid(x) < t
+        xs = np.nextafter(np.float32(lf), np.float32(-np.inf)) - np.arange(0, 2000, dtype=np.float32) * np.float32(1e-5)
+        assert all(O.sigmoid(float(x)) < np.float32(t) for x in xs[:200])
+        assert O.sigmoid(lf) < np.float32(t)

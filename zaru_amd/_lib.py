@@ -52,6 +52,8 @@ SIGNATURES = [
     ("zr_detection_candidates_async", _I, [_P, _P, _U32, _U32, _U32, _F, _U32, _P, _P, _P]),
     ("zr_session_stats", _I, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(_SZ)]),
     ("zr_plan_describe", _I, [_P, _SZ, _P, _SZ, _P, _SZ, C.POINTER(_SZ)]),
+    ("zr_profile_enable", _I, [_P, _I]),
+    ("zr_profile_read", _I, [_P, _P, _SZ, C.POINTER(_SZ)]),
     ("zr_last_error", C.c_char_p, []),
     ("zr_device_count", _I, [C.POINTER(_I)]),
     ("zr_malloc", _I, [C.POINTER(_P), _SZ]),

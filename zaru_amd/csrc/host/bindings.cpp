@@ -1,0 +1,308 @@
+// bindings.cpp -- pybind11 module `_zaru_host`: the reference's host-side API (Detector,
+// NonMaxSuppression, Estimator, LandmarkTracker, Rect/RotatedRect, ...) over the C ABI, so
+// that parity tests read like the reference's own #[test]s.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "detection.h"
+#include "landmark.h"
+#include "pipeline.h"
+
+namespace py = pybind11;
+using namespace zh;
+
+namespace {
+
+Image host_image(const py::array_t<uint8_t, py::array::c_style> &a) {
+    if (a.ndim() != 3 || a.shape(2) != 4) throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "image must be HxWx4 uint8 RGBA");
+    Image im;
+    im.rgba = a.data();
+    im.height = (uint32_t)a.shape(0);
+    im.width = (uint32_t)a.shape(1);
+    im.row_stride = (uint64_t)a.shape(1) * 4;
+    im.on_device = false;
+    return im;
+}
+
+py::tuple rect_tuple(const Rect &r) {
+    return py::make_tuple(r.center().x, r.center().y, r.width(), r.height());
+}
+
+py::dict estimate_dict(const Estimate &e) {
+    py::dict d;
+    py::array_t<float> p({(py::ssize_t)e.size(), (py::ssize_t)3});
+    std::memcpy(p.mutable_data(), e.positions.data(), e.positions.size() * 4);
+    d["landmarks"] = p;
+    d["confidence"] = e.confidence;
+    d["raw_handedness"] = e.raw_handedness;
+    return d;
+}
+
+DetectorNetwork detector_net(const std::string &name) {
+    if (name == "face") return DetectorNetwork::short_range_face();
+    if (name == "palm") return DetectorNetwork::palm_lite();
+    throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "detector network must be 'face' or 'palm'");
+}
+
+LandmarkNetwork landmark_net(const std::string &name) {
+    if (name == "facemesh") return LandmarkNetwork::face_mesh_v1();
+    if (name == "hand") return LandmarkNetwork::hand_lite();
+    throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "landmark network must be 'facemesh' or 'hand'");
+}
+
+// Detector::detect_impl after inference on raw outputs (detection.rs:231-267)
+std::vector<Detection> detect_post(const std::string &net, py::array_t<float, py::array::c_style> boxes,
+                                   py::array_t<float, py::array::c_style> logits, uint32_t img_w,
+                                   uint32_t img_h, float thresh, float iou) {
+    DetectorNetwork dn = detector_net(net);
+    const uint32_t s = dn.kind == NetworkKind::FaceDetectionShortRange ? 128 : 192;
+    if ((size_t)logits.size() != dn.anchors().size() || (size_t)boxes.size() != dn.anchors().size() * dn.params)
+        throw ZaruError(ZR_ERR_SHAPE, "raw outputs do not match the network's anchors");
+    std::vector<Detection> raw;
+    dn.extract(boxes.data(), logits.data(), thresh, s, s, raw);
+    NonMaxSuppression nms;
+    nms.set_iou_thresh(iou);
+    auto out = nms.process(raw);
+    Rect rect;
+    letterbox_view(img_w, img_h, AspectRatio::of(s, s), &rect);
+    map_detections(out, rect, s);
+    return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_zaru_host, m) {
+    m.doc() = "Host-side mirror of Zaru's detection/landmark API over the MI355X C ABI";
+    py::register_exception<ZaruError>(m, "ZaruError", PyExc_RuntimeError);
+
+    py::class_<Rect>(m, "Rect")
+        .def_static("from_center", &Rect::from_center)
+        .def_static("from_top_left", &Rect::from_top_left)
+        .def_static("bounding", [](const std::vector<std::pair<float, float>> &pts) -> py::object {
+            std::vector<Vec2> v;
+            for (auto &p : pts) v.push_back({p.first, p.second});
+            Rect r;
+            if (!Rect::bounding(v.data(), v.size(), r)) return py::none();
+            return py::cast(r);
+        })
+        .def_property_readonly("center", [](const Rect &r) { return py::make_tuple(r.center().x, r.center().y); })
+        .def_property_readonly("size", [](const Rect &r) { return py::make_tuple(r.width(), r.height()); })
+        .def("width", &Rect::width)
+        .def("height", &Rect::height)
+        .def("x", &Rect::x)
+        .def("y", &Rect::y)
+        .def("area", &Rect::area)
+        .def("top_left", [](const Rect &r) { return py::make_tuple(r.top_left().x, r.top_left().y); })
+        .def("scale", &Rect::scale)
+        .def("grow_rel", &Rect::grow_rel)
+        .def("grow_to_fit_aspect", [](const Rect &r, uint32_t w, uint32_t h) { return r.grow_to_fit_aspect(AspectRatio::of(w, h)); })
+        .def("iou", &Rect::iou)
+        .def("intersection", [](const Rect &a, const Rect &b) -> py::object {
+            Rect o;
+            if (!a.intersection(b, o)) return py::none();
+            return py::cast(o);
+        })
+        .def("intersection_area", &Rect::intersection_area)
+        .def("contains_point", [](const Rect &r, float x, float y) { return r.contains_point({x, y}); })
+        .def("tuple", &rect_tuple)
+        .def("__eq__", &Rect::operator==)
+        .def("__repr__", [](const Rect &r) {
+            return "Rect @ (" + std::to_string(r.center().x) + "," + std::to_string(r.center().y) + ")/" +
+                   std::to_string(r.width()) + "x" + std::to_string(r.height());
+        });
+
+    py::class_<RotatedRect>(m, "RotatedRect")
+        .def(py::init<Rect, float>(), py::arg("rect"), py::arg("radians") = 0.f)
+        .def_static("bounding", [](float rad, const std::vector<std::pair<float, float>> &pts) -> py::object {
+            std::vector<Vec2> v;
+            for (auto &p : pts) v.push_back({p.first, p.second});
+            RotatedRect r;
+            if (!RotatedRect::bounding(rad, v.data(), v.size(), 2, r)) return py::none();
+            return py::cast(r);
+        })
+        .def("rect", &RotatedRect::rect)
+        .def("rotation_radians", &RotatedRect::rotation_radians)
+        .def("grow_rel", &RotatedRect::grow_rel)
+        .def("transform_in", [](const RotatedRect &r, float x, float y) { auto p = r.transform_in({x, y}); return py::make_tuple(p.x, p.y); })
+        .def("transform_out", [](const RotatedRect &r, float x, float y) { auto p = r.transform_out({x, y}); return py::make_tuple(p.x, p.y); })
+        .def("contains_point", [](const RotatedRect &r, float x, float y) { return r.contains_point({x, y}); });
+
+    py::class_<ViewData>(m, "ViewData")
+        .def_static("full", &ViewData::full)
+        .def("view", [](const ViewData &v, const RotatedRect &r) { return v.view(r); })
+        .def("view_rect", [](const ViewData &v, const Rect &r) { return v.view(RotatedRect(r, 0.f)); })
+        .def_property_readonly("rect", [](const ViewData &v) { return v.rect; })
+        .def("local_rect", &ViewData::local_rect)
+        .def("zr_view", [](const ViewData &v) {
+            auto z = to_zr_view(v);
+            return py::make_tuple(z.cx, z.cy, z.w, z.h, z.rad);
+        });
+
+    m.def("signed_angle_to", [](float ax, float ay, float bx, float by) { return signed_angle_to({ax, ay}, {bx, by}); });
+    m.def("sigmoid", &sigmoid);
+    m.def("letterbox_view", [](uint32_t w, uint32_t h, uint32_t aw, uint32_t ah) {
+        Rect r;
+        ViewData v = letterbox_view(w, h, AspectRatio::of(aw, ah), &r);
+        return py::make_tuple(v, r);
+    });
+    m.def("candidate_logit_floor", &candidate_logit_floor);
+
+    py::class_<Detection>(m, "Detection")
+        .def(py::init([](float conf, const Rect &r) {
+                 Detection d;
+                 d.confidence = conf;
+                 d.rect = r;
+                 return d;
+             }), py::arg("confidence"), py::arg("rect"))
+        .def("confidence", [](const Detection &d) { return d.confidence; })
+        .def("angle", [](const Detection &d) { return d.angle; })
+        .def("bounding_rect", [](const Detection &d) { return d.rect; })
+        .def_readonly("anchor", &Detection::anchor)
+        .def("keypoints", [](const Detection &d) {
+            std::vector<std::pair<float, float>> k;
+            for (auto &p : d.keypoints) k.push_back({p.x, p.y});
+            return k;
+        });
+
+    py::enum_<SuppressionMode>(m, "SuppressionMode")
+        .value("Remove", SuppressionMode::Remove)
+        .value("Average", SuppressionMode::Average);
+
+    py::class_<NonMaxSuppression>(m, "NonMaxSuppression")
+        .def(py::init<>())
+        .def("set_iou_thresh", &NonMaxSuppression::set_iou_thresh)
+        .def("set_mode", &NonMaxSuppression::set_mode)
+        .def("process", [](const NonMaxSuppression &n, std::vector<Detection> dets) { return n.process(dets); });
+
+    m.def("detect_post", &detect_post, py::arg("network"), py::arg("boxes"), py::arg("logits"),
+          py::arg("img_w"), py::arg("img_h"), py::arg("thresh") = Detector::DEFAULT_THRESHOLD,
+          py::arg("iou") = NonMaxSuppression::DEFAULT_IOU_THRESH);
+    m.def("anchors", [](const std::string &net) {
+        auto a = detector_net(net).anchors();
+        py::array_t<float> o({(py::ssize_t)a.size(), (py::ssize_t)2});
+        std::memcpy(o.mutable_data(), a.data(), a.size() * 8);
+        return o;
+    });
+    m.def("set_models_dir", &set_models_dir);
+
+    py::class_<Detector>(m, "Detector")
+        .def(py::init([](const std::string &net, int device) { return new Detector(detector_net(net), device); }),
+             py::arg("network") = "face", py::arg("device") = 0)
+        .def("set_threshold", &Detector::set_threshold)
+        .def("set_nms_iou", [](Detector &d, float t) { d.nms_mut().set_iou_thresh(t); })
+        .def("set_nms_mode", [](Detector &d, SuppressionMode m) { d.nms_mut().set_mode(m); })
+        .def("input_width", &Detector::input_width)
+        .def("detect", [](Detector &d, py::array_t<uint8_t, py::array::c_style> img) {
+            return d.detect(host_image(img));
+        });
+
+    py::class_<Estimator>(m, "Estimator")
+        .def(py::init([](const std::string &net, int device) { return new Estimator(landmark_net(net), device); }),
+             py::arg("network") = "facemesh", py::arg("device") = 0)
+        .def("input_width", &Estimator::input_width)
+        .def("estimate", [](Estimator &e, py::array_t<uint8_t, py::array::c_style> img, const ViewData &v) {
+            Image im = host_image(img);
+            return estimate_dict(e.estimate(im, v));
+        })
+        .def("estimate_image", [](Estimator &e, py::array_t<uint8_t, py::array::c_style> img) {
+            Image im = host_image(img);
+            return estimate_dict(e.estimate(im, ViewData::full(im.width, im.height)));
+        })
+        .def("angle_radians", [](const Estimator &e, py::array_t<float, py::array::c_style> lm) {
+            Estimate est;
+            est.positions.assign(lm.data(), lm.data() + lm.size());
+            return estimate_angle(e.network(), est);
+        });
+
+    py::class_<LandmarkTracker>(m, "LandmarkTracker")
+        .def(py::init([](const std::string &net, int device) {
+                 return new LandmarkTracker(Estimator(landmark_net(net), device));
+             }), py::arg("network") = "facemesh", py::arg("device") = 0)
+        .def("set_roi", [](LandmarkTracker &t, const RotatedRect &r) { t.set_roi(r); })
+        .def("set_roi_rect", [](LandmarkTracker &t, const Rect &r) { t.set_roi(RotatedRect(r, 0.f)); })
+        .def("set_loss_threshold", &LandmarkTracker::set_loss_threshold)
+        .def("set_roi_padding", &LandmarkTracker::set_roi_padding)
+        .def("roi", [](const LandmarkTracker &t) -> py::object {
+            if (!t.roi()) return py::none();
+            return py::cast(*t.roi());
+        })
+        .def("track", [](LandmarkTracker &t, py::array_t<uint8_t, py::array::c_style> img) -> py::object {
+            auto r = t.track(host_image(img));
+            if (!r) return py::none();
+            py::dict d = estimate_dict(r->estimate);
+            d["view_rect"] = r->view_rect;
+            d["updated_roi"] = r->updated_roi;
+            return d;
+        });
+
+    py::class_<DetectTrackPipeline>(m, "DetectTrackPipeline")
+        .def(py::init([](const std::string &kind, int device, int threads, uint32_t max_rois) {
+                 PipelineConfig c = kind == "hand" ? PipelineConfig::hand() : PipelineConfig::face();
+                 if (kind != "hand" && kind != "face")
+                     throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "pipeline kind must be 'face' or 'hand'");
+                 c.max_rois_per_frame = max_rois;
+                 return new DetectTrackPipeline(c, device, threads);
+             }), py::arg("kind") = "face", py::arg("device") = 0, py::arg("threads") = 8,
+             py::arg("max_rois_per_frame") = 8)
+        // frames: list of (device ptr, width, height, row_stride); forced: per frame list of
+        // (cx, cy, w, h, rad) ROIs used when the frame has no detection
+        .def("run", [](DetectTrackPipeline &p, const std::vector<std::tuple<uint64_t, uint32_t, uint32_t, uint64_t>> &frames,
+                       const std::vector<std::vector<std::tuple<float, float, float, float, float>>> &forced) {
+            std::vector<Image> im;
+            for (auto &f : frames) {
+                Image i;
+                i.rgba = reinterpret_cast<const uint8_t *>(std::get<0>(f));
+                i.width = std::get<1>(f);
+                i.height = std::get<2>(f);
+                i.row_stride = std::get<3>(f);
+                i.on_device = true;
+                im.push_back(i);
+            }
+            std::vector<std::vector<RotatedRect>> fr(forced.size());
+            for (size_t k = 0; k < forced.size(); k++)
+                for (auto &t : forced[k])
+                    fr[k].push_back(RotatedRect(Rect::from_center(std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t)), std::get<4>(t)));
+            py::gil_scoped_release nogil;
+            p.run(im, fr);
+        })
+        .def("detections", [](const DetectTrackPipeline &p) { return p.detections(); })
+        .def("num_rois", [](const DetectTrackPipeline &p) { return p.rois().size(); })
+        .def("roi", [](const DetectTrackPipeline &p, size_t i) {
+            const RoiResult &r = p.rois().at(i);
+            py::dict d = estimate_dict(r.result.estimate);
+            d["frame"] = r.frame;
+            d["from_detection"] = r.from_detection;
+            d["tracked"] = r.tracked;
+            d["roi"] = r.roi;
+            d["view_rect"] = r.result.view_rect;
+            d["updated_roi"] = r.result.updated_roi;
+            d["next_roi"] = r.next_roi;
+            return d;
+        })
+        .def("times", [](const DetectTrackPipeline &p) {
+            const StageTimes &t = p.times();
+            py::dict d;
+            d["detect_gpu_ms"] = t.detect_gpu_ms;
+            d["decode_nms_ms"] = t.decode_nms_ms;
+            d["landmark_gpu_ms"] = t.landmark_gpu_ms;
+            d["map_ms"] = t.map_ms;
+            d["total_ms"] = t.total_ms;
+            d["frames"] = t.frames;
+            d["detections"] = t.detections;
+            d["rois"] = t.rois;
+            d["tracked"] = t.tracked;
+            return d;
+        })
+        .def("stats", [](const DetectTrackPipeline &p) {
+            py::dict d;
+            d["detector_bytes_per_image"] = p.detector_bytes_per_image();
+            d["landmarker_bytes_per_image"] = p.landmarker_bytes_per_image();
+            d["detector_flops_per_image"] = p.detector_flops_per_image();
+            d["landmarker_flops_per_image"] = p.landmarker_flops_per_image();
+            return d;
+        })
+        .def("stream", [](const DetectTrackPipeline &p) { return reinterpret_cast<uint64_t>(p.stream()); })
+        .def("profile", &DetectTrackPipeline::profile)
+        .def("profile_read", &DetectTrackPipeline::profile_read);
+}

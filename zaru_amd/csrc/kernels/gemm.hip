@@ -99,14 +99,18 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmParams P) {
 }
 
 template <int MT>
-static void launch_mt(const GemmParams &p, dim3 grid, hipStream_t s) {
+static const char *launch_mt(const GemmParams &p, dim3 grid, hipStream_t s) {
+    static const char *names[2][5] = {
+        {"", "gemm_kernel<1,false>", "gemm_kernel<2,false>", "gemm_kernel<3,false>", "gemm_kernel<4,false>"},
+        {"", "gemm_kernel<1,true>", "gemm_kernel<2,true>", "gemm_kernel<3,true>", "gemm_kernel<4,true>"}};
     if (p.KK > 1)
         hipLaunchKernelGGL((gemm_kernel<MT, true>), grid, dim3(256), 0, s, p);
     else
         hipLaunchKernelGGL((gemm_kernel<MT, false>), grid, dim3(256), 0, s, p);
+    return names[p.KK > 1][MT];
 }
 
-void launch_gemm(const GemmParams &p, hipStream_t s) {
+const char *launch_gemm(const GemmParams &p, hipStream_t s) {
     const int mtiles = p.Mpad / 32;
     const int bx = (p.ncols + 127) / 128;
     // Largest M tile (operand reuse) that still leaves >= 2 workgroups per CU of parallelism.
@@ -115,10 +119,10 @@ void launch_gemm(const GemmParams &p, hipStream_t s) {
     if (mt > mtiles) mt = mtiles;
     dim3 grid(bx, (mtiles + mt - 1) / mt);
     switch (mt) {
-    case 4: launch_mt<4>(p, grid, s); break;
-    case 3: launch_mt<3>(p, grid, s); break;
-    case 2: launch_mt<2>(p, grid, s); break;
-    default: launch_mt<1>(p, grid, s); break;
+    case 4: return launch_mt<4>(p, grid, s);
+    case 3: return launch_mt<3>(p, grid, s);
+    case 2: return launch_mt<2>(p, grid, s);
+    default: return launch_mt<1>(p, grid, s);
     }
 }
 

@@ -35,10 +35,11 @@ __global__ __launch_bounds__(256) void elt_kernel(const EltParams P) {
     }
 }
 
-void launch_elt(const EltParams &p, hipStream_t s) {
+const char *launch_elt(const EltParams &p, hipStream_t s) {
     const int HW = p.H * p.W;
     dim3 grid(p.C * p.N, std::min((HW + 255) / 256, 64));
     hipLaunchKernelGGL(elt_kernel, grid, dim3(256), 0, s, p);
+    return "elt_kernel";
 }
 
 // ------------------------------------------------------------------ resize (bilinear)
@@ -66,10 +67,11 @@ __global__ __launch_bounds__(256) void resize_kernel(const ResizeParams P) {
     }
 }
 
-void launch_resize(const ResizeParams &p, hipStream_t s) {
+const char *launch_resize(const ResizeParams &p, hipStream_t s) {
     const int n = p.OH * p.OW;
     dim3 grid(p.in.C * p.N, std::min((n + 255) / 256, 64));
     hipLaunchKernelGGL(resize_kernel, grid, dim3(256), 0, s, p);
+    return "resize_kernel";
 }
 
 // ------------------------------------------------------------------ global average pool
@@ -88,9 +90,10 @@ __global__ __launch_bounds__(256) void gap_kernel(const GapParams P, int planes)
     if (lane == 0) P.out[(int64_t)n * P.o_sN + (int64_t)c * P.o_sC] = s / (float)HW;
 }
 
-void launch_gap(const GapParams &p, hipStream_t s) {
+const char *launch_gap(const GapParams &p, hipStream_t s) {
     const int planes = p.in.C * p.N;
     hipLaunchKernelGGL(gap_kernel, dim3((planes + 3) / 4), dim3(256), 0, s, p, planes);
+    return "gap_kernel";
 }
 
 // ------------------------------------------------------------------ detection candidates
@@ -120,8 +123,9 @@ __global__ __launch_bounds__(256) void cand_kernel(const CandParams P) {
     if (threadIdx.x == 0) P.count[n] = cnt;
 }
 
-void launch_candidates(const CandParams &p, hipStream_t s) {
+const char *launch_candidates(const CandParams &p, hipStream_t s) {
     hipLaunchKernelGGL(cand_kernel, dim3(p.N), dim3(256), 0, s, p);
+    return "cand_kernel";
 }
 
 }  // namespace zr

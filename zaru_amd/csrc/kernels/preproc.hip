@@ -56,10 +56,11 @@ __global__ __launch_bounds__(256) void preproc_kernel(const PreprocParams P) {
     o[2 * P.o_sC] = (float)((rgba >> 16) & 0xFF) * P.adjust + P.lo;
 }
 
-void launch_preproc(const PreprocParams &p, hipStream_t s) {
-    if (p.nviews == 0) return;
+const char *launch_preproc(const PreprocParams &p, hipStream_t s) {
+    if (p.nviews == 0) return "preproc_kernel";
     dim3 grid((p.OW * p.OH + 255) / 256, p.nviews);
     hipLaunchKernelGGL(preproc_kernel, grid, dim3(256), 0, s, p);
+    return "preproc_kernel";
 }
 
 }  // namespace zr

@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256) void dw_kernel(const DwParams P, int TH) {
 }
 
 template <int K, int S>
-static void dw_launch(const DwParams &p, hipStream_t s) {
+static const char *dw_launch(const DwParams &p, hipStream_t s) {
     const int planes = p.in.C * p.N;
     // ~1024 outputs per 256-thread workgroup; tiny planes use a single wave
     int th = p.OH;
@@ -61,13 +61,14 @@ static void dw_launch(const DwParams &p, hipStream_t s) {
     const size_t lds = sizeof(float) * (size_t)win * rin;
     dim3 grid(planes, (p.OH + th - 1) / th);
     hipLaunchKernelGGL((dw_kernel<K, S>), grid, dim3(threads), lds, s, p, th);
+    return K == 3 ? (S == 1 ? "dw_kernel<3,1>" : "dw_kernel<3,2>") : (S == 1 ? "dw_kernel<5,1>" : "dw_kernel<5,2>");
 }
 
-void launch_dw(const DwParams &p, hipStream_t s) {
-    if (p.k == 3 && p.stride == 1) dw_launch<3, 1>(p, s);
-    else if (p.k == 3 && p.stride == 2) dw_launch<3, 2>(p, s);
-    else if (p.k == 5 && p.stride == 1) dw_launch<5, 1>(p, s);
-    else if (p.k == 5 && p.stride == 2) dw_launch<5, 2>(p, s);
+const char *launch_dw(const DwParams &p, hipStream_t s) {
+    if (p.k == 3 && p.stride == 1) return dw_launch<3, 1>(p, s);
+    if (p.k == 3 && p.stride == 2) return dw_launch<3, 2>(p, s);
+    if (p.k == 5 && p.stride == 1) return dw_launch<5, 1>(p, s);
+    return dw_launch<5, 2>(p, s);
 }
 
 // ------------------------------------------------------------------ dense direct conv
@@ -131,7 +132,7 @@ __global__ __launch_bounds__(256) void direct_kernel(const DirectParams P, int C
     }
 }
 
-void launch_direct(const DirectParams &p, hipStream_t s) {
+const char *launch_direct(const DirectParams &p, hipStream_t s) {
     const int rin = (DTH - 1) * p.stride + p.kh, win = (DTW - 1) * p.stride + p.kw;
     const int kk = p.kh * p.kw;
     int cc = p.in.C;
@@ -141,6 +142,7 @@ void launch_direct(const DirectParams &p, hipStream_t s) {
     const int tiles = ((p.OH + DTH - 1) / DTH) * ((p.OW + DTW - 1) / DTW);
     dim3 grid(tiles, p.N, (p.Cout + DCO - 1) / DCO);
     hipLaunchKernelGGL(direct_kernel, grid, dim3(256), lds, s, p, cc);
+    return "direct_kernel";
 }
 
 }  // namespace zr

@@ -784,10 +784,12 @@ Plane plane_of(const TRef &r, const Plan &plan, const Binding &b) {
 
 }  // namespace
 
-void run_plan(const Plan &plan, const Binding &b, hipStream_t stream) {
+void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook *hook) {
     const float *W = b.weights;
     for (const Step &s : plan.steps) {
         Resolved out = resolve(s.out, plan, b);
+        const char *kname = nullptr;
+        if (hook) hook->before(stream);
         switch (s.kind) {
         case S_GEMM: {
             Resolved x = resolve(s.in, plan, b);
@@ -821,7 +823,7 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream) {
             g.o_sN = out.sN;
             g.o_sC = out.sC;
             g.o_sP = out.sP;
-            launch_gemm(g, stream);
+            kname = launch_gemm(g, stream);
             break;
         }
         case S_DW: {
@@ -840,7 +842,7 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream) {
             d.w = W + s.w_off;
             d.bias = W + s.b_off;
             d.act = act_of(s.pre, W);
-            launch_dw(d, stream);
+            kname = launch_dw(d, stream);
             break;
         }
         case S_DIRECT: {
@@ -861,7 +863,7 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream) {
             d.w = W + s.w_off;
             d.bias = W + s.b_off;
             d.act = act_of(s.pre, W);
-            launch_direct(d, stream);
+            kname = launch_direct(d, stream);
             break;
         }
         case S_ELT: {
@@ -877,7 +879,7 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream) {
             e.H = s.out.H;
             e.W = s.out.W;
             e.act = act_of(s.pre, W);
-            launch_elt(e, stream);
+            kname = launch_elt(e, stream);
             break;
         }
         case S_RESIZE: {
@@ -891,7 +893,7 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream) {
             r.OW = s.out.W;
             r.scale_y = s.scale_y;
             r.scale_x = s.scale_x;
-            launch_resize(r, stream);
+            kname = launch_resize(r, stream);
             break;
         }
         case S_GAP: {
@@ -901,10 +903,11 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream) {
             g.o_sN = out.sN;
             g.o_sC = out.sC;
             g.N = b.N;
-            launch_gap(g, stream);
+            kname = launch_gap(g, stream);
             break;
         }
         }
+        if (hook) hook->after(stream, kname, s.bytes * b.N, s.flops * b.N);
     }
 }
 

@@ -79,6 +79,14 @@ struct Binding {
     const float *weights = nullptr;
 };
 
-void run_plan(const Plan &plan, const Binding &b, hipStream_t stream);
+// Optional per-launch hook (profiling): called before and after every kernel launch with the
+// step index, the launched kernel's symbol (after only) and the launch's algorithmic work.
+struct LaunchHook {
+    virtual ~LaunchHook() = default;
+    virtual void before(hipStream_t s) = 0;
+    virtual void after(hipStream_t s, const char *kernel, double bytes, double flops) = 0;
+};
+
+void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook *hook = nullptr);
 
 }  // namespace zr

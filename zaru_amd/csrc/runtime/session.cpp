@@ -94,9 +94,52 @@ zr::ViewDesc make_view(const zr_view &v, uint32_t frame) {
     return d;
 }
 
+// Per-launch HIP-event timing (zr_profile_*): events are recorded on the launching stream
+// around every kernel, so the measured durations come from the timed work itself.
+struct Profiler final : zr::LaunchHook {
+    struct Rec {
+        const char *kernel;
+        double bytes, flops;
+        hipEvent_t a, b;
+    };
+    std::mutex mu;
+    bool on = false;
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> pool;
+    hipEvent_t pending = nullptr;
+
+    hipEvent_t get() {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+    void before(hipStream_t s) override {
+        pending = get();
+        (void)hipEventRecord(pending, s);
+    }
+    void after(hipStream_t s, const char *k, double bytes, double flops) override {
+        hipEvent_t e = get();
+        (void)hipEventRecord(e, s);
+        recs.push_back({k, bytes, flops, pending, e});
+    }
+    ~Profiler() {
+        for (auto &r : recs) {
+            (void)hipEventDestroy(r.a);
+            (void)hipEventDestroy(r.b);
+        }
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+};
+
 }  // namespace
 
 struct zr_session {
+    Profiler prof;
     int device = 0;
     zr::Plan plan;
     float *weights = nullptr;
@@ -160,7 +203,11 @@ int enqueue(zr_session *s, Ctx *c, int N, const float *input, int64_t in_sN, int
     b.outputs = outs;
     b.arena = c->arena;
     b.weights = s->weights;
-    zr::run_plan(s->plan, b, stream);
+    {
+        std::unique_lock<std::mutex> pl(s->prof.mu, std::defer_lock);
+        if (s->prof.on) pl.lock();
+        zr::run_plan(s->plan, b, stream, s->prof.on ? &s->prof : nullptr);
+    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->done, stream));
     return ZR_OK;
@@ -310,6 +357,54 @@ int zr_plan_describe(const uint8_t *onnx, size_t len, const uint32_t *out_sel, s
     return ZR_OK;
 }
 
+int zr_profile_enable(zr_session *s, int enable) {
+    if (int rc = check_session(s)) return rc;
+    std::lock_guard<std::mutex> g(s->prof.mu);
+    s->prof.on = enable != 0;
+    return ZR_OK;
+}
+
+int zr_profile_read(zr_session *s, char *buf, size_t cap, size_t *needed) {
+    if (int rc = check_session(s)) return rc;
+    std::lock_guard<std::mutex> g(s->prof.mu);
+    struct Agg {
+        size_t n = 0;
+        double ms = 0, bytes = 0, flops = 0;
+    };
+    std::vector<std::pair<std::string, Agg>> aggs;
+    for (auto &r : s->prof.recs) {
+        HIP_TRY(hipEventSynchronize(r.b));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));
+        auto it = std::find_if(aggs.begin(), aggs.end(), [&](auto &p) { return p.first == r.kernel; });
+        if (it == aggs.end()) {
+            aggs.push_back({r.kernel, Agg{}});
+            it = aggs.end() - 1;
+        }
+        it->second.n++;
+        it->second.ms += ms;
+        it->second.bytes += r.bytes;
+        it->second.flops += r.flops;
+        s->prof.pool.push_back(r.a);
+        s->prof.pool.push_back(r.b);
+    }
+    s->prof.recs.clear();
+    std::string t;
+    char line[256];
+    for (auto &a : aggs) {
+        snprintf(line, sizeof line, "%s %zu %.6f %.0f %.0f\n", a.first.c_str(), a.second.n, a.second.ms,
+                 a.second.bytes, a.second.flops);
+        t += line;
+    }
+    if (needed) *needed = t.size() + 1;
+    if (buf && cap) {
+        size_t n = std::min(cap - 1, t.size());
+        memcpy(buf, t.data(), n);
+        buf[n] = 0;
+    }
+    return ZR_OK;
+}
+
 int zr_session_stats(const zr_session *s, double *bytes, double *flops, size_t *launches) {
     if (int rc = check_session(s)) return rc;
     if (bytes) *bytes = s->plan.bytes_per_image;
@@ -376,7 +471,14 @@ static int views_common(zr_session *s, Ctx *c, const zr_frame *frames, size_t nf
     p.out = c->input;
     p.o_sN = hw;                    // CNHW straight into the plan's input layout
     p.o_sC = hw * (int64_t)nv;
-    zr::launch_preproc(p, stream);
+    {
+        std::unique_lock<std::mutex> pl(s->prof.mu, std::defer_lock);
+        if (s->prof.on) pl.lock();
+        if (s->prof.on) s->prof.before(stream);
+        const char *k = zr::launch_preproc(p, stream);
+        // algorithmic bytes: RGBA gather 4 B + 3 f32 writes per output position
+        if (s->prof.on) s->prof.after(stream, k, 16.0 * (double)hw * nv, 0.0);
+    }
     HIP_TRY(hipGetLastError());
     return enqueue(s, c, (int)nv, c->input, hw, hw * (int64_t)nv, outs, stream);
 }

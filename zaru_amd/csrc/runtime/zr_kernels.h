@@ -143,14 +143,14 @@ struct CandParams {
     float *rec;              // [N][cap][2 + D]
 };
 
-// launchers (kernels/*.hip)
-void launch_gemm(const GemmParams &p, hipStream_t s);
-void launch_dw(const DwParams &p, hipStream_t s);
-void launch_direct(const DirectParams &p, hipStream_t s);
-void launch_elt(const EltParams &p, hipStream_t s);
-void launch_resize(const ResizeParams &p, hipStream_t s);
-void launch_gap(const GapParams &p, hipStream_t s);
-void launch_preproc(const PreprocParams &p, hipStream_t s);
-void launch_candidates(const CandParams &p, hipStream_t s);
+// launchers (kernels/*.hip); each returns the symbol of the kernel it launched
+const char *launch_gemm(const GemmParams &p, hipStream_t s);
+const char *launch_dw(const DwParams &p, hipStream_t s);
+const char *launch_direct(const DirectParams &p, hipStream_t s);
+const char *launch_elt(const EltParams &p, hipStream_t s);
+const char *launch_resize(const ResizeParams &p, hipStream_t s);
+const char *launch_gap(const GapParams &p, hipStream_t s);
+const char *launch_preproc(const PreprocParams &p, hipStream_t s);
+const char *launch_candidates(const CandParams &p, hipStream_t s);
 
 }  // namespace zr
