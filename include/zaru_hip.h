@@ -127,10 +127,16 @@ const char *zr_last_error(void);
 int zr_device_count(int *n);
 int zr_malloc(void **p, size_t bytes);
 int zr_free(void *p);
+int zr_host_alloc(void **p, size_t bytes); /* page-locked host memory (truly async copies) */
+int zr_host_free(void *p);
 int zr_memcpy_async(void *dst, const void *src, size_t bytes, int kind, void *hip_stream);
 int zr_stream_create(void **stream);
 int zr_stream_destroy(void *stream);
 int zr_stream_synchronize(void *stream);
+int zr_event_create(void **event);
+int zr_event_destroy(void *event);
+int zr_event_record(void *event, void *stream);
+int zr_event_synchronize(void *event);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,118 @@
+"""The reference's host-level call chains through the HIP backend (zaru_amd.host):
+Detector::detect, Estimator::estimate, LandmarkTracker::track and the batched
+DetectTrackPipeline, checked against the reference's own expectations and against each other."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def codes_image(codes):
+    """An RGBA image whose identity view reproduces the committed network input exactly."""
+    c, h, w = codes.shape
+    img = np.full((h, w, 4), 255, np.uint8)
+    img[..., :3] = codes.transpose(1, 2, 0)
+    return img
+
+
+@pytest.fixture(scope="module")
+def H():
+    import zaru_amd.host as H
+    return H
+
+
+def test_detector_detects_face(H, golden_dir, kat):
+    """face/detection.rs:164-173 via Detector::detect on the HIP backend."""
+    g = np.load(os.path.join(golden_dir, "sad_linus_face.npz"))
+    img = codes_image(g["codes"])
+    det = H.Detector("face")
+    dets = det.detect(img)
+    m = kat["models"]["detects_face"]
+    assert len(dets) >= 1
+    assert dets[0].confidence() >= m["min_conf"]
+    assert abs(math.degrees(dets[0].angle())) < m["max_abs_angle_deg"]
+    # same selection as the oracle decode of the f64 outputs (128 px space: identity letterbox)
+    want = O.detect_post(O.FACE, g["regressors"][0], g["classificators"][0], 128, 128, 128, 128)
+    assert len(want) == len(dets)
+    assert np.allclose(dets[0].bounding_rect().tuple(), want[0].rect.tuple(), atol=1e-2)
+
+
+def test_estimator_facemesh(H, golden_dir, kat):
+    g = np.load(os.path.join(golden_dir, "sad_linus_mesh.npz"))
+    m = kat["models"]["facemesh"]
+    est = H.Estimator("facemesh")
+    for i, case in enumerate(m["cases"]):
+        r = est.estimate_image(codes_image(g["codes"][i]))
+        assert r["confidence"] > m["min_conf"]
+        ang = math.degrees(est.angle_radians(r["landmarks"]))
+        assert abs(ang - case["expect_deg"]) < m["angle_tol_deg"]
+        l2 = np.sqrt(((r["landmarks"][:, :2] - g["landmarks"][i][:, :2]) ** 2).sum(-1)).max()
+        assert l2 <= 1e-3, l2
+
+
+def test_tracker_follows_face(H, golden_dir):
+    """LandmarkTracker::track (landmark.rs:463-501): seeded with the whole crop, tracking holds
+    and the next ROI stays on the face."""
+    g = np.load(os.path.join(golden_dir, "sad_linus_mesh.npz"))
+    img = codes_image(g["codes"][0])
+    t = H.LandmarkTracker("facemesh")
+    t.set_roi_rect(H.Rect.from_top_left(0, 0, 192, 192))
+    r = t.track(img)
+    assert r is not None and r["confidence"] > 0.9
+    roi = t.roi()
+    assert roi is not None
+    cx, cy = roi.rect().center
+    assert 40 < cx < 150 and 40 < cy < 150
+    # a second pass from the updated ROI keeps tracking
+    assert t.track(img) is not None
+
+
+def test_tracker_loses_on_noise(H):
+    rng = np.random.default_rng(1)
+    img = rng.integers(0, 256, size=(300, 300, 4), dtype=np.uint8)
+    t = H.LandmarkTracker("facemesh")
+    t.set_roi_rect(H.Rect.from_top_left(20, 20, 200, 200))
+    r = t.track(img)
+    if r is None:
+        assert t.roi() is None  # lost -> ROI cleared (landmark.rs:468-477)
+
+
+@pytest.mark.parametrize("kind", ["face", "hand"])
+def test_pipeline_equals_per_frame_api(H, kind):
+    """Batched DetectTrackPipeline == Detector::detect + one LandmarkTracker pass per frame,
+    bit for bit (every kernel's per-image result is independent of the batch)."""
+    from zaru_amd._lib import DeviceBuffer
+    rng = np.random.default_rng(21 if kind == "face" else 22)
+    frames = [rng.integers(0, 256, size=(h, w, 4), dtype=np.uint8)
+              for h, w in ((240, 320), (360, 640), (300, 300), (480, 200), (256, 256))]
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "sad_linus_face.npz"))
+    frames[2][:128, :128, :3] = g["codes"].transpose(1, 2, 0)  # one real face
+    bufs = [DeviceBuffer.from_array(f) for f in frames]
+    flist = [(b.ptr, f.shape[1], f.shape[0], f.shape[1] * 4) for b, f in zip(bufs, frames)]
+    forced = [[(f.shape[1] / 2, f.shape[0] / 2, 150.0, 150.0, 0.3 if kind == "hand" else 0.0)]
+              for f in frames]
+    p = H.DetectTrackPipeline(kind, 0, 4, 4)
+    p.run(flist, forced)
+    det = H.Detector("face" if kind == "face" else "palm")
+    for f, img in enumerate(frames):
+        want = det.detect(img)
+        got = p.detections()[f]
+        assert len(got) == len(want)
+        for a, b in zip(got, want):
+            assert a.confidence() == b.confidence() and a.angle() == b.angle()
+            assert a.bounding_rect() == b.bounding_rect()
+    for i in range(p.num_rois()):
+        r = p.roi(i)
+        t = H.LandmarkTracker("facemesh" if kind == "face" else "hand")
+        t.set_roi_padding(0.3 if kind == "face" else 0.4)
+        t.set_roi(r["roi"])
+        res = t.track(frames[r["frame"]])
+        assert (res is not None) == r["tracked"]
+        if res is not None:
+            assert np.array_equal(res["landmarks"], r["landmarks"])
+            assert res["updated_roi"].rect() == r["updated_roi"].rect()

@@ -58,10 +58,16 @@ SIGNATURES = [
     ("zr_device_count", _I, [C.POINTER(_I)]),
     ("zr_malloc", _I, [C.POINTER(_P), _SZ]),
     ("zr_free", _I, [_P]),
+    ("zr_host_alloc", _I, [C.POINTER(_P), _SZ]),
+    ("zr_host_free", _I, [_P]),
     ("zr_memcpy_async", _I, [_P, _P, _SZ, _I, _P]),
     ("zr_stream_create", _I, [C.POINTER(_P)]),
     ("zr_stream_destroy", _I, [_P]),
     ("zr_stream_synchronize", _I, [_P]),
+    ("zr_event_create", _I, [C.POINTER(_P)]),
+    ("zr_event_destroy", _I, [_P]),
+    ("zr_event_record", _I, [_P, _P]),
+    ("zr_event_synchronize", _I, [_P]),
 ]
 
 

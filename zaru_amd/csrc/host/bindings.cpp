@@ -237,14 +237,18 @@ PYBIND11_MODULE(_zaru_host, m) {
         });
 
     py::class_<DetectTrackPipeline>(m, "DetectTrackPipeline")
-        .def(py::init([](const std::string &kind, int device, int threads, uint32_t max_rois) {
+        .def(py::init([](const std::string &kind, int device, int threads, uint32_t max_rois,
+                         uint32_t sub_batches, bool stream_per_sub_batch) {
                  PipelineConfig c = kind == "hand" ? PipelineConfig::hand() : PipelineConfig::face();
                  if (kind != "hand" && kind != "face")
                      throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "pipeline kind must be 'face' or 'hand'");
                  c.max_rois_per_frame = max_rois;
+                 c.sub_batches = sub_batches;
+                 c.stream_per_sub_batch = stream_per_sub_batch;
                  return new DetectTrackPipeline(c, device, threads);
              }), py::arg("kind") = "face", py::arg("device") = 0, py::arg("threads") = 8,
-             py::arg("max_rois_per_frame") = 8)
+             py::arg("max_rois_per_frame") = 8, py::arg("sub_batches") = 2,
+             py::arg("stream_per_sub_batch") = true)
         // frames: list of (device ptr, width, height, row_stride); forced: per frame list of
         // (cx, cy, w, h, rad) ROIs used when the frame has no detection
         .def("run", [](DetectTrackPipeline &p, const std::vector<std::tuple<uint64_t, uint32_t, uint32_t, uint64_t>> &frames,
@@ -265,6 +269,29 @@ PYBIND11_MODULE(_zaru_host, m) {
                     fr[k].push_back(RotatedRect(Rect::from_center(std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t)), std::get<4>(t)));
             py::gil_scoped_release nogil;
             p.run(im, fr);
+        })
+        .def("set_frames", [](DetectTrackPipeline &p, const std::vector<std::tuple<uint64_t, uint32_t, uint32_t, uint64_t>> &frames,
+                              const std::vector<std::vector<std::tuple<float, float, float, float, float>>> &forced) {
+            std::vector<Image> im;
+            for (auto &f : frames) {
+                Image i;
+                i.rgba = reinterpret_cast<const uint8_t *>(std::get<0>(f));
+                i.width = std::get<1>(f);
+                i.height = std::get<2>(f);
+                i.row_stride = std::get<3>(f);
+                i.on_device = true;
+                im.push_back(i);
+            }
+            std::vector<std::vector<RotatedRect>> fr(forced.size());
+            for (size_t k = 0; k < forced.size(); k++)
+                for (auto &t : forced[k])
+                    fr[k].push_back(RotatedRect(Rect::from_center(std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t)), std::get<4>(t)));
+            p.set_frames(std::move(im), std::move(fr));
+        })
+        .def("run_frames", [](DetectTrackPipeline &p) {
+            py::gil_scoped_release nogil;
+            p.run_frames();
+            return p.rois().size();
         })
         .def("detections", [](const DetectTrackPipeline &p) { return p.detections(); })
         .def("num_rois", [](const DetectTrackPipeline &p) { return p.rois().size(); })

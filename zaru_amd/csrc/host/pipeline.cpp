@@ -106,9 +106,25 @@ DetectTrackPipeline::DetectTrackPipeline(PipelineConfig cfg, int device, int thr
       lm_cnn_(network_cnn(cfg_.landmarker.kind, device)), pool_(threads) {
     nms_.set_iou_thresh(cfg_.nms_iou);
     check(zr_stream_create(&stream_));
+    // every slot enqueues on the one pipeline stream (the GPU runs the kernels back to back,
+    // so per-kernel timings stay clean); the host waits on per-slot events instead
+    for (uint32_t i = 0; i < std::max(1u, cfg_.sub_batches); i++) {
+        slots_.push_back(std::make_unique<Slot>());
+        Slot &s = *slots_.back();
+        if (cfg_.stream_per_sub_batch && i > 0) check(zr_stream_create(&s.stream));
+        else s.stream = stream_;
+        check(zr_event_create(&s.ev_det));
+        check(zr_event_create(&s.ev_lm));
+    }
 }
 
 DetectTrackPipeline::~DetectTrackPipeline() {
+    for (auto &s : slots_) {
+        if (s->stream) zr_stream_synchronize(s->stream);
+        if (s->stream && s->stream != stream_) zr_stream_destroy(s->stream);
+        if (s->ev_det) zr_event_destroy(s->ev_det);
+        if (s->ev_lm) zr_event_destroy(s->ev_lm);
+    }
     if (stream_) zr_stream_destroy(stream_);
 }
 
@@ -148,6 +164,11 @@ std::string DetectTrackPipeline::profile_read() {
     return out;
 }
 
+void DetectTrackPipeline::set_frames(std::vector<Image> frames, std::vector<std::vector<RotatedRect>> forced) {
+    frames_ = std::move(frames);
+    forced_ = std::move(forced);
+}
+
 namespace {
 using clk = std::chrono::steady_clock;
 double ms_since(clk::time_point t) {
@@ -155,75 +176,72 @@ double ms_since(clk::time_point t) {
 }
 }  // namespace
 
-void DetectTrackPipeline::run(const std::vector<Image> &frames,
-                              const std::vector<std::vector<RotatedRect>> &forced) {
-    const auto t0 = clk::now();
-    const size_t B = frames.size();
-    times_ = StageTimes{};
-    times_.frames = B;
-    dets_.assign(B, {});
-    rois_.clear();
-    if (B == 0) return;
+// stage 1 (enqueue only): letterbox views -> detector -> candidate compaction -> D2H
+void DetectTrackPipeline::stage_detect(Slot &s, const std::vector<Image> &frames) {
+    const Cnn &dc = *det_cnn_;
+    const uint32_t A = (uint32_t)cfg_.detector.anchors().size(), D = (uint32_t)cfg_.detector.params;
+    const uint32_t cap = cfg_.candidate_cap, rec_w = 2 + D;
+    const size_t n = s.nf;
+    s.zf.resize(n);
+    s.letterbox.resize(n);
+    std::vector<zr_view> zv(n);
+    std::vector<uint32_t> vf(n);
+    for (size_t i = 0; i < n; i++) {
+        const Image &im = frames[s.f0 + i];
+        if (!im.on_device) throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "pipeline frames must be device-resident");
+        s.zf[i] = zr_frame{im.rgba, im.width, im.height, im.row_stride};
+        zv[i] = to_zr_view(letterbox_view(im.width, im.height, dc.aspect(), &s.letterbox[i]));
+        vf[i] = (uint32_t)i;
+    }
+    s.d_boxes.resize(n * A * D);
+    s.d_logits.resize(n * A);
+    s.d_count.resize(n);
+    s.d_rec.resize(n * cap * rec_w);
+    float *douts[2] = {s.d_boxes.ptr, s.d_logits.ptr};
+    dc.estimate_async(s.zf, zv, vf, douts, s.stream);
+    check(zr_detection_candidates_async(s.d_logits.ptr, s.d_boxes.ptr, (uint32_t)n, A, D,
+                                        candidate_logit_floor(cfg_.det_threshold), cap, s.d_count.ptr,
+                                        s.d_rec.ptr, s.stream));
+    s.h_count.resize(n);
+    s.h_rec.resize(n * cap * rec_w);
+    check(zr_memcpy_async(s.h_count.data(), s.d_count.ptr, n * sizeof(int32_t), 1, s.stream));
+    check(zr_memcpy_async(s.h_rec.data(), s.d_rec.ptr, n * cap * rec_w * sizeof(float), 1, s.stream));
+    check(zr_event_record(s.ev_det, s.stream));
+}
 
+// stage 2 (after stage 1 completed): exact decode + NMS + map (detection.rs:231-267), the
+// ROI views of every tracked object, then enqueue the landmark network over all of them
+void DetectTrackPipeline::stage_decode_and_rois(Slot &s, const std::vector<Image> &frames,
+                                                const std::vector<std::vector<RotatedRect>> &forced) {
     const Cnn &dc = *det_cnn_;
     const uint32_t din_w = dc.input_width(), din_h = dc.input_height();
-    const auto &anchors = cfg_.detector.anchors();
-    const uint32_t A = (uint32_t)anchors.size(), D = (uint32_t)cfg_.detector.params;
+    const uint32_t A = (uint32_t)cfg_.detector.anchors().size(), D = (uint32_t)cfg_.detector.params;
     const uint32_t cap = cfg_.candidate_cap, rec_w = 2 + D;
-
-    // ---- stage 1: letterbox views of every frame -> detector (one batched launch chain)
-    std::vector<zr_frame> zf(B);
-    std::vector<zr_view> zv(B);
-    std::vector<uint32_t> vf(B);
-    std::vector<Rect> letterbox(B);
-    for (size_t f = 0; f < B; f++) {
-        if (!frames[f].on_device) throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "pipeline frames must be device-resident");
-        zf[f] = zr_frame{frames[f].rgba, frames[f].width, frames[f].height, frames[f].row_stride};
-        zv[f] = to_zr_view(letterbox_view(frames[f].width, frames[f].height, dc.aspect(), &letterbox[f]));
-        vf[f] = (uint32_t)f;
-    }
-    d_boxes_.resize((size_t)B * A * D);
-    d_logits_.resize((size_t)B * A);
-    d_count_.resize(B);
-    d_rec_.resize((size_t)B * cap * rec_w);
-    float *douts[2] = {d_boxes_.ptr, d_logits_.ptr};
-    dc.estimate_async(zf, zv, vf, douts, stream_);
-    const float floor = candidate_logit_floor(cfg_.det_threshold);
-    check(zr_detection_candidates_async(d_logits_.ptr, d_boxes_.ptr, (uint32_t)B, A, D, floor, cap,
-                                        d_count_.ptr, d_rec_.ptr, stream_));
-    h_count_.resize(B);
-    h_rec_.resize((size_t)B * cap * rec_w);
-    check(zr_memcpy_async(h_count_.data(), d_count_.ptr, B * sizeof(int32_t), 1, stream_));
-    check(zr_memcpy_async(h_rec_.data(), d_rec_.ptr, h_rec_.size() * sizeof(float), 1, stream_));
-    check(zr_stream_synchronize(stream_));
-    times_.detect_gpu_ms = ms_since(t0);
-
-    // ---- stage 2: exact decode + NMS + map to image coordinates (host, per frame)
-    const auto t1 = clk::now();
-    std::vector<size_t> overflow;
-    for (size_t f = 0; f < B; f++)
-        if ((uint32_t)h_count_[f] > cap) overflow.push_back(f);
-    std::vector<std::vector<float>> full_boxes(B), full_logits(B);
-    for (size_t f : overflow) {  // rare: more candidates than slots -> copy that frame whole
-        full_boxes[f].resize((size_t)A * D);
-        full_logits[f].resize(A);
-        check(zr_memcpy_async(full_boxes[f].data(), d_boxes_.ptr + f * A * D, (size_t)A * D * 4, 1, stream_));
-        check(zr_memcpy_async(full_logits[f].data(), d_logits_.ptr + f * A, (size_t)A * 4, 1, stream_));
-    }
-    if (!overflow.empty()) check(zr_stream_synchronize(stream_));
+    const size_t n = s.nf;
+    std::vector<std::vector<float>> full_boxes(n), full_logits(n);
+    bool overflow = false;
+    for (size_t i = 0; i < n; i++)
+        if ((uint32_t)s.h_count[i] > cap) {  // rare: more candidates than slots -> whole frame
+            overflow = true;
+            full_boxes[i].resize((size_t)A * D);
+            full_logits[i].resize(A);
+            check(zr_memcpy_async(full_boxes[i].data(), s.d_boxes.ptr + i * A * D, (size_t)A * D * 4, 1, s.stream));
+            check(zr_memcpy_async(full_logits[i].data(), s.d_logits.ptr + i * A, (size_t)A * 4, 1, s.stream));
+        }
+    if (overflow) check(zr_stream_synchronize(s.stream));
     const float thresh = cfg_.det_threshold;
-    pool_.parallel_for(B, [&](size_t f) {
+    pool_.parallel_for(n, [&](size_t i) {
         std::vector<Detection> raw;
-        if (!full_logits[f].empty()) {
-            cfg_.detector.extract(full_boxes[f].data(), full_logits[f].data(), thresh, din_w, din_h, raw);
+        if (!full_logits[i].empty()) {
+            cfg_.detector.extract(full_boxes[i].data(), full_logits[i].data(), thresh, din_w, din_h, raw);
         } else {
-            const int n = h_count_[f];
-            const float *rec = &h_rec_[f * cap * rec_w];
-            std::vector<std::pair<uint32_t, int>> order;  // restore anchor order
-            for (int i = 0; i < n; i++) {
+            const int cnt = s.h_count[i];
+            const float *rec = &s.h_rec[i * cap * rec_w];
+            std::vector<std::pair<uint32_t, int>> order;  // restore anchor order (extract_outputs)
+            for (int k = 0; k < cnt; k++) {
                 uint32_t a;
-                std::memcpy(&a, &rec[i * rec_w], 4);
-                order.push_back({a, i});
+                std::memcpy(&a, &rec[k * rec_w], 4);
+                order.push_back({a, k});
             }
             std::sort(order.begin(), order.end());
             for (auto &o : order) {
@@ -233,19 +251,19 @@ void DetectTrackPipeline::run(const std::vector<Image> &frames,
                 raw.push_back(cfg_.detector.decode(o.first, r + 2, conf, din_w, din_h));
             }
         }
-        dets_[f] = nms_.process(raw);
-        map_detections(dets_[f], letterbox[f], din_w);
+        auto &dets = dets_[s.f0 + i];
+        dets = nms_.process(raw);
+        map_detections(dets, s.letterbox[i], din_w);
     });
-    times_.decode_nms_ms = ms_since(t1);
 
-    // ---- stage 3: ROIs -> landmark network (one batched launch chain over all ROIs)
-    const auto t2 = clk::now();
     const Cnn &lc = *lm_cnn_;
     const AspectRatio la = lc.aspect();
-    std::vector<zr_view> rv;
-    std::vector<uint32_t> rf;
-    std::vector<Rect> local_rect;
-    for (size_t f = 0; f < B; f++) {
+    s.rv.clear();
+    s.rf.clear();
+    s.local_rect.clear();
+    s.roi0 = rois_.size();
+    for (size_t i = 0; i < n; i++) {
+        const size_t f = s.f0 + i;
         std::vector<std::pair<RotatedRect, bool>> seeds;
         for (const auto &d : dets_[f]) {
             if (seeds.size() >= cfg_.max_rois_per_frame) break;
@@ -258,58 +276,97 @@ void DetectTrackPipeline::run(const std::vector<Image> &frames,
                 seeds.push_back({r, false});
             }
         const ViewData full = ViewData::full(frames[f].width, frames[f].height);
-        for (const auto &s : seeds) {
+        for (const auto &sd : seeds) {
             RoiResult r;
             r.frame = (uint32_t)f;
-            r.from_detection = s.second;
-            r.roi = s.first;
+            r.from_detection = sd.second;
+            r.roi = sd.first;
             // LandmarkTracker::track_impl (landmark.rs:465-467) + Estimator (landmark.rs:320-323)
-            r.result.view_rect = s.first.grow_to_fit_aspect(la);
+            r.result.view_rect = sd.first.grow_to_fit_aspect(la);
             const ViewData view = full.view(r.result.view_rect);
             const Rect rect = view.local_rect().grow_to_fit_aspect(la);
-            rv.push_back(to_zr_view(view.view(RotatedRect(rect, 0.f))));
-            rf.push_back((uint32_t)f);
-            local_rect.push_back(rect);
+            s.rv.push_back(to_zr_view(view.view(RotatedRect(rect, 0.f))));
+            s.rf.push_back((uint32_t)i);
+            s.local_rect.push_back(rect);
             rois_.push_back(r);
         }
     }
-    const size_t R = rois_.size();
-    times_.rois = R;
-    for (auto &d : dets_) times_.detections += d.size();
+    s.nroi = rois_.size() - s.roi0;
+    if (s.nroi == 0) return;
     const size_t nout = lc.nn().num_outputs();
-    if (R > 0) {
-        std::vector<float *> lptr(nout);
-        for (size_t i = 0; i < nout; i++) {
-            d_lm_[i].resize((size_t)lc.nn().output_per_image(i) * R);
-            lptr[i] = d_lm_[i].ptr;
-        }
-        lc.estimate_async(zf, rv, rf, lptr.data(), stream_);
-        for (size_t i = 0; i < nout; i++) {
-            h_lm_[i].resize((size_t)lc.nn().output_per_image(i) * R);
-            check(zr_memcpy_async(h_lm_[i].data(), lptr[i], h_lm_[i].size() * 4, 1, stream_));
-        }
-        check(zr_stream_synchronize(stream_));
+    std::vector<float *> lptr(nout);
+    for (size_t k = 0; k < nout; k++) {
+        s.d_lm[k].resize((size_t)lc.nn().output_per_image(k) * s.nroi);
+        lptr[k] = s.d_lm[k].ptr;
     }
-    times_.landmark_gpu_ms = ms_since(t2);
+    lc.estimate_async(s.zf, s.rv, s.rf, lptr.data(), s.stream);
+    for (size_t k = 0; k < nout; k++) {
+        const size_t cnt = (size_t)lc.nn().output_per_image(k) * s.nroi;
+        s.h_lm[k].resize(cnt);
+        check(zr_memcpy_async(s.h_lm[k].data(), lptr[k], cnt * 4, 1, s.stream));
+    }
+    check(zr_event_record(s.ev_lm, s.stream));
+}
 
-    // ---- stage 4: extract + Estimator map-out + tracker update (host, per ROI)
-    const auto t3 = clk::now();
+// stage 4 (after the landmark outputs arrived): extract + Estimator map-out + tracker update
+void DetectTrackPipeline::stage_map(Slot &s) {
+    const Cnn &lc = *lm_cnn_;
     const uint32_t lin_w = lc.input_width();
-    std::atomic<size_t> tracked{0};
-    pool_.parallel_for(R, [&](size_t i) {
-        RoiResult &r = rois_[i];
+    const size_t nout = lc.nn().num_outputs();
+    pool_.parallel_for(s.nroi, [&](size_t i) {
+        RoiResult &r = rois_[s.roi0 + i];
         const float *outs[4];
-        for (size_t k = 0; k < nout; k++) outs[k] = &h_lm_[k][i * lc.nn().output_per_image(k)];
+        for (size_t k = 0; k < nout; k++) outs[k] = &s.h_lm[k][i * lc.nn().output_per_image(k)];
         Estimate e;
         extract_landmarks(cfg_.landmarker, outs, e);
-        map_estimate(e, local_rect[i], lin_w);
+        map_estimate(e, s.local_rect[i], lin_w);
         r.tracked = tracker_update(cfg_.landmarker, r.roi, r.result.view_rect, cfg_.loss_threshold,
                                    cfg_.roi_padding, e, r.result, r.next_roi);
         if (!r.tracked) r.result.estimate = std::move(e);
-        else tracked++;
     });
-    times_.tracked = tracked.load();
-    times_.map_ms = ms_since(t3);
+}
+
+void DetectTrackPipeline::run(const std::vector<Image> &frames,
+                              const std::vector<std::vector<RotatedRect>> &forced) {
+    const auto t0 = clk::now();
+    const size_t B = frames.size();
+    times_ = StageTimes{};
+    times_.frames = B;
+    dets_.assign(B, {});
+    rois_.clear();
+    if (B == 0) return;
+    // split into sub-batches (software pipeline): GPU det(k+1) overlaps host decode(k), GPU
+    // landmarks(k) overlaps host decode(k+1), host map(k) overlaps GPU landmarks(k+1)
+    const size_t S = std::min<size_t>(slots_.size(), B);
+    size_t f0 = 0;
+    for (size_t k = 0; k < S; k++) {
+        Slot &s = *slots_[k];
+        s.f0 = f0;
+        s.nf = B / S + (k < B % S ? 1 : 0);
+        f0 += s.nf;
+        stage_detect(s, frames);
+    }
+    for (size_t k = 0; k < S; k++) {
+        Slot &s = *slots_[k];
+        const auto t = clk::now();
+        check(zr_event_synchronize(s.ev_det));
+        times_.detect_gpu_ms += ms_since(t);
+        const auto t1 = clk::now();
+        stage_decode_and_rois(s, frames, forced);
+        times_.decode_nms_ms += ms_since(t1);
+    }
+    for (size_t k = 0; k < S; k++) {
+        Slot &s = *slots_[k];
+        const auto t = clk::now();
+        if (s.nroi) check(zr_event_synchronize(s.ev_lm));
+        times_.landmark_gpu_ms += ms_since(t);
+        const auto t1 = clk::now();
+        stage_map(s);
+        times_.map_ms += ms_since(t1);
+    }
+    times_.rois = rois_.size();
+    for (auto &d : dets_) times_.detections += d.size();
+    for (auto &r : rois_) times_.tracked += r.tracked ? 1 : 0;
     times_.total_ms = ms_since(t0);
 }
 

@@ -61,6 +61,12 @@ struct PipelineConfig {
     float loss_threshold = LandmarkTracker::DEFAULT_LOSS_THRESHOLD;
     uint32_t max_rois_per_frame = 8;
     uint32_t candidate_cap = 64;  // device compaction slots per frame (overflow -> full copy)
+    // the batch runs as this many sub-batches on their own streams, software-pipelined so
+    // that the host decode / mapping of one overlaps the GPU work of the next
+    uint32_t sub_batches = 2;
+    // give each sub-batch its own HIP stream (kernels of different sub-batches may then run
+    // concurrently on the GPU); false = one stream, kernels strictly back to back
+    bool stream_per_sub_batch = true;
     static PipelineConfig face();  // BlazeFace -> FaceMesh V1 (config 3)
     static PipelineConfig hand();  // BlazePalm lite -> hand landmark lite (config 4)
 };
@@ -87,20 +93,44 @@ class DetectTrackPipeline {
     void profile(bool on);
     std::string profile_read();  // "<net>/<kernel> <launches> <total_ms> <bytes> <flops>" lines
 
+    // keep a frame set (and its forced ROIs) resident in the pipeline, so repeated runs over
+    // the same device frames pay no per-call argument conversion
+    void set_frames(std::vector<Image> frames, std::vector<std::vector<RotatedRect>> forced);
+    void run_frames() { run(frames_, forced_); }
+
   private:
+    // one software-pipeline slot: a contiguous range of frames with its own stream/buffers
+    struct Slot {
+        size_t f0 = 0, nf = 0;
+        void *stream = nullptr;
+        void *ev_det = nullptr, *ev_lm = nullptr;  // stage-1 / stage-3 outputs on the host
+        DeviceArray<float> d_boxes, d_logits, d_rec, d_lm[4];
+        DeviceArray<int32_t> d_count;
+        PinnedArray<float> h_rec, h_lm[4];
+        PinnedArray<int32_t> h_count;
+        std::vector<zr_frame> zf;
+        std::vector<Rect> letterbox, local_rect;
+        std::vector<zr_view> rv;
+        std::vector<uint32_t> rf;
+        size_t roi0 = 0, nroi = 0;
+    };
+    void stage_detect(Slot &s, const std::vector<Image> &frames);
+    void stage_decode_and_rois(Slot &s, const std::vector<Image> &frames,
+                               const std::vector<std::vector<RotatedRect>> &forced);
+    void stage_map(Slot &s);
+
     PipelineConfig cfg_;
     int device_;
     std::shared_ptr<const Cnn> det_cnn_, lm_cnn_;
     NonMaxSuppression nms_;
     ThreadPool pool_;
     void *stream_ = nullptr;
-    DeviceArray<float> d_boxes_, d_logits_, d_rec_, d_lm_[4];
-    DeviceArray<int32_t> d_count_;
-    std::vector<float> h_rec_, h_lm_[4];
-    std::vector<int32_t> h_count_;
+    std::vector<std::unique_ptr<Slot>> slots_;
     std::vector<std::vector<Detection>> dets_;
     std::vector<RoiResult> rois_;
     StageTimes times_;
+    std::vector<Image> frames_;
+    std::vector<std::vector<RotatedRect>> forced_;
 };
 
 }  // namespace zh

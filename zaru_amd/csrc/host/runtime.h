@@ -51,6 +51,31 @@ struct DeviceArray {
     }
 };
 
+// Page-locked host array: device<->host copies into it stay asynchronous.
+template <typename T>
+struct PinnedArray {
+    T *ptr = nullptr;
+    size_t n = 0;
+    PinnedArray() = default;
+    PinnedArray(const PinnedArray &) = delete;
+    PinnedArray &operator=(const PinnedArray &) = delete;
+    ~PinnedArray() {
+        if (ptr) zr_host_free(ptr);
+    }
+    void resize(size_t count) {
+        if (count <= n) return;
+        if (ptr) zr_host_free(ptr);
+        ptr = nullptr;
+        void *p = nullptr;
+        check(zr_host_alloc(&p, count * sizeof(T)));
+        ptr = static_cast<T *>(p);
+        n = count;
+    }
+    T &operator[](size_t i) { return ptr[i]; }
+    const T &operator[](size_t i) const { return ptr[i]; }
+    T *data() { return ptr; }
+};
+
 // NeuralNetwork (crates/zaru/src/nn/mod.rs:365-539) = one HIP session.
 class NeuralNetwork {
   public:

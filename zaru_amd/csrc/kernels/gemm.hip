@@ -98,6 +98,155 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmParams P) {
         }
 }
 
+// ---------------------------------------------------------------- LDS-tiled variant
+// For the common case of a CNHW activation (X is then a plain row-major [K][ncols] matrix with
+// leading dimension x_sC) with ncols % 4 == 0: both operands are staged through LDS with
+// 16-byte loads (one wave instruction moves a whole 1 KiB row segment), double-buffered with
+// the next K-chunk's loads in flight during the current chunk's MFMAs.  Each wave owns NT
+// 32-column tiles x MT 32-row tiles, so every A fragment feeds NT MFMAs and every B fragment MT.
+// Block -> tile mapping is XCD-aware: the M-blocks of one column tile are 8 launch slots apart,
+// i.e. on the same XCD under round-robin dispatch, so their shared X tile is an L2 hit.
+constexpr int TKC = 16;  // K rows per stage
+
+template <int MT, int NT>
+__global__ __launch_bounds__(256) void gemm_tiled_kernel(const GemmParams P, int mblocks, int nct) {
+    constexpr int BN = 4 * NT * 32, MR = MT * 32;
+    constexpr int XV = TKC * BN / 4 / 256;  // float4 of X staged per thread per chunk
+    constexpr int WV = (TKC * MR / 4 + 255) / 256;
+    __shared__ __attribute__((aligned(16))) float sX[2][TKC][BN];
+    __shared__ __attribute__((aligned(16))) float sW[2][TKC][MR];
+
+    int ct, mb;
+    if (mblocks == 1) {
+        ct = blockIdx.x;
+        mb = 0;
+    } else {
+        const int g = blockIdx.x / (8 * mblocks), r = blockIdx.x - g * 8 * mblocks;
+        mb = r >> 3;
+        ct = g * 8 + (r & 7);
+    }
+    if (ct >= nct) return;  // whole workgroup, before any barrier
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kh = lane >> 5, col = lane & 31;
+    const int j0 = ct * BN, m0 = mb * MR;
+    const int nchunks = (P.K + TKC - 1) / TKC;
+
+    float4 rx[XV], rw[WV];
+    auto load = [&](int kc) {
+#pragma unroll
+        for (int u = 0; u < XV; ++u) {
+            const int i = tid + 256 * u, row = i / (BN / 4), c4 = i - row * (BN / 4);
+            const int k = kc + row, j = j0 + 4 * c4;
+            rx[u] = (k < P.K && j < P.ncols)
+                        ? *reinterpret_cast<const float4 *>(P.x + (int64_t)k * P.x_sC + j)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < WV; ++u) {
+            const int i = tid + 256 * u, row = i / (MR / 4), c4 = i - row * (MR / 4);
+            const int k = kc + row;
+            rw[u] = (i < TKC * MR / 4 && k < P.K && m0 + 4 * c4 < P.Mpad)
+                        ? *reinterpret_cast<const float4 *>(P.wt + (int64_t)k * P.Mpad + m0 + 4 * c4)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < XV; ++u) {
+            const int i = tid + 256 * u, row = i / (BN / 4), c4 = i - row * (BN / 4);
+            *reinterpret_cast<float4 *>(&sX[buf][row][4 * c4]) = rx[u];
+        }
+#pragma unroll
+        for (int u = 0; u < WV; ++u) {
+            const int i = tid + 256 * u, row = i / (MR / 4), c4 = i - row * (MR / 4);
+            if (i < TKC * MR / 4) *reinterpret_cast<float4 *>(&sW[buf][row][4 * c4]) = rw[u];
+        }
+    };
+
+    f32x16 acc[MT][NT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int u = 0; u < NT; ++u)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
+
+    load(0);
+    store(0);
+    __syncthreads();
+    for (int c = 0; c < nchunks; ++c) {
+        const int buf = c & 1;
+        if (c + 1 < nchunks) load((c + 1) * TKC);
+#pragma unroll
+        for (int s = 0; s < TKC / 2; ++s) {
+            float a[MT], b[NT];
+#pragma unroll
+            for (int t = 0; t < MT; ++t) a[t] = sW[buf][2 * s + kh][t * 32 + col];
+#pragma unroll
+            for (int u = 0; u < NT; ++u) b[u] = sX[buf][2 * s + kh][(wave * NT + u) * 32 + col];
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+#pragma unroll
+                for (int u = 0; u < NT; ++u)
+                    acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t], b[u], acc[t][u], 0, 0, 0);
+        }
+        if (c + 1 < nchunks) store(buf ^ 1);
+        __syncthreads();
+    }
+
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+        const int j = j0 + (wave * NT + u) * 32 + col;
+        if (j >= P.ncols) continue;
+        const int n = j / P.P, q = j - n * P.P;
+        float *ob = P.out + (int64_t)n * P.o_sN + (int64_t)q * P.o_sP;
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+                if (m >= P.M) continue;
+                float v = apply_act(P.pre, acc[t][u][r] + P.bias[m], m);
+                if (P.res_mode != 0 && m < P.r_C) {
+                    const float *rb = P.r + (int64_t)n * P.r_sN + (int64_t)m * P.r_sC;
+                    float rv;
+                    if (P.res_mode == 1) {
+                        rv = rb[q];
+                    } else {
+                        const int y = q / P.out_W, x = q - y * P.out_W;
+                        const float *s0 = rb + (int64_t)(2 * y) * P.r_W + 2 * x;
+                        rv = fmaxf(fmaxf(s0[0], s0[1]), fmaxf(s0[P.r_W], s0[P.r_W + 1]));
+                    }
+                    v += rv;
+                }
+                ob[(int64_t)m * P.o_sC] = apply_act(P.post, v, m);
+            }
+    }
+}
+
+template <int MT, int NT>
+static const char *launch_tiled(const GemmParams &p, hipStream_t s) {
+    constexpr int BN = 4 * NT * 32;
+    const int nct = (p.ncols + BN - 1) / BN;
+    const int mblocks = (p.Mpad + MT * 32 - 1) / (MT * 32);
+    const int nblk = mblocks == 1 ? nct : ((nct + 7) / 8) * 8 * mblocks;
+    hipLaunchKernelGGL((gemm_tiled_kernel<MT, NT>), dim3(nblk), dim3(256), 0, s, p, mblocks, nct);
+    static const char *names[2][5] = {
+        {"", "gemm_tiled_kernel<1,1>", "gemm_tiled_kernel<2,1>", "gemm_tiled_kernel<3,1>", "gemm_tiled_kernel<4,1>"},
+        {"", "gemm_tiled_kernel<1,2>", "gemm_tiled_kernel<2,2>", "gemm_tiled_kernel<3,2>", "gemm_tiled_kernel<4,2>"}};
+    return names[NT - 1][MT];
+}
+
+template <int NT>
+static const char *launch_tiled_nt(const GemmParams &p, int mt, hipStream_t s) {
+    switch (mt) {
+    case 4: return launch_tiled<4, NT>(p, s);
+    case 3: return launch_tiled<3, NT>(p, s);
+    case 2: return launch_tiled<2, NT>(p, s);
+    default: return launch_tiled<1, NT>(p, s);
+    }
+}
+
 template <int MT>
 static const char *launch_mt(const GemmParams &p, dim3 grid, hipStream_t s) {
     static const char *names[2][5] = {
@@ -112,6 +261,17 @@ static const char *launch_mt(const GemmParams &p, dim3 grid, hipStream_t s) {
 
 const char *launch_gemm(const GemmParams &p, hipStream_t s) {
     const int mtiles = p.Mpad / 32;
+    // LDS-tiled path: X must be a row-major [K][ncols] matrix with 16-B aligned rows
+    const bool rowmajor = p.KK == 1 && p.x_sN == p.P && (p.x_sC % 4) == 0 && (p.ncols % 4) == 0 &&
+                          ((uintptr_t)p.x % 16) == 0 && (p.Mpad % 4) == 0 && ((uintptr_t)p.wt % 16) == 0;
+    if (rowmajor) {
+        int mt = std::min(4, mtiles);
+        const int nt = p.ncols >= 256 * 256 ? 2 : 1;  // wide tiles once there are >= 256 of them
+        const int bn = 4 * nt * 32;
+        // keep >= ~2 workgroups per CU: trade M-tile reuse for parallelism on small problems
+        while (mt > 1 && (int64_t)((p.ncols + bn - 1) / bn) * ((mtiles + mt - 1) / mt) < 512) --mt;
+        return nt == 2 ? launch_tiled_nt<2>(p, mt, s) : launch_tiled_nt<1>(p, mt, s);
+    }
     const int bx = (p.ncols + 127) / 128;
     // Largest M tile (operand reuse) that still leaves >= 2 workgroups per CU of parallelism.
     int mt = 4;

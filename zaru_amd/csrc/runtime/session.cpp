@@ -47,6 +47,9 @@ struct Ctx {
     zr::ViewDesc *views = nullptr;
     zr::FrameDesc *frames = nullptr;
     size_t views_cap = 0, frames_cap = 0;
+    zr::ViewDesc *h_views = nullptr;  // pinned host staging of the descriptors
+    zr::FrameDesc *h_frames = nullptr;
+    size_t h_views_cap = 0, h_frames_cap = 0;
     std::vector<float *> outs;  // device outputs for the synchronous entry points
     std::vector<size_t> outs_floats;
 
@@ -57,6 +60,8 @@ struct Ctx {
         (void)hipFree(image);
         (void)hipFree(views);
         (void)hipFree(frames);
+        (void)hipHostFree(h_views);
+        (void)hipHostFree(h_frames);
         for (auto p : outs) (void)hipFree(p);
         if (done) (void)hipEventDestroy(done);
         if (stream) (void)hipStreamDestroy(stream);
@@ -149,12 +154,16 @@ struct zr_session {
 
     Ctx *acquire() {
         std::lock_guard<std::mutex> g(pool_mu);
-        // prefer an idle context; grow the pool up to 8 under contention
+        // prefer a context whose previous work has completed on the GPU (its workspace and
+        // pinned staging may then be rewritten without any wait); grow the pool up to 8
         for (size_t i = 0; i < pool.size(); i++) {
             Ctx *c = pool[(next + i) % pool.size()].get();
             if (c->mu.try_lock()) {
-                next = (next + i + 1) % pool.size();
-                return c;
+                if (hipEventQuery(c->done) == hipSuccess) {
+                    next = (next + i + 1) % pool.size();
+                    return c;
+                }
+                c->mu.unlock();
             }
         }
         if (pool.size() < 8) {
@@ -170,6 +179,7 @@ struct zr_session {
         Ctx *c = pool[next].get();
         next = (next + 1) % pool.size();
         c->mu.lock();
+        (void)hipEventSynchronize(c->done);  // all 8 busy: reuse the oldest once it is done
         return c;
     }
 
@@ -231,22 +241,29 @@ int upload_views(Ctx *c, const zr_frame *frames, size_t nf, const zr_view *views
                  const uint32_t *view_frame, size_t nv, hipStream_t stream) {
     if (int rc = grow(c->views, c->views_cap, nv ? nv : 1)) return rc;
     if (int rc = grow(c->frames, c->frames_cap, nf ? nf : 1)) return rc;
-    std::vector<zr::ViewDesc> vd(nv);
+    // pinned staging: the context was acquired idle (or waited for), so it is free to rewrite,
+    // and the copies stay asynchronous (a pageable source would block the host on the stream)
+    if (c->h_views_cap < nv || c->h_frames_cap < nf) {
+        (void)hipHostFree(c->h_views);
+        (void)hipHostFree(c->h_frames);
+        c->h_views_cap = nv + nv / 2 + 64;
+        c->h_frames_cap = nf + nf / 2 + 64;
+        HIP_TRY(hipHostMalloc((void **)&c->h_views, c->h_views_cap * sizeof(zr::ViewDesc)));
+        HIP_TRY(hipHostMalloc((void **)&c->h_frames, c->h_frames_cap * sizeof(zr::FrameDesc)));
+    }
     for (size_t i = 0; i < nv; i++) {
         const uint32_t f = view_frame ? view_frame[i] : 0;
         if (f >= nf) return set_err(ZR_ERR_INVALID_ARGUMENT, "view_frame index out of range");
-        vd[i] = make_view(views[i], f);
+        c->h_views[i] = make_view(views[i], f);
     }
-    std::vector<zr::FrameDesc> fd(nf);
     for (size_t i = 0; i < nf; i++) {
-        fd[i].rgba = frames[i].rgba;
-        fd[i].w = frames[i].width;
-        fd[i].h = frames[i].height;
-        fd[i].stride = frames[i].row_stride;
+        c->h_frames[i].rgba = frames[i].rgba;
+        c->h_frames[i].w = frames[i].width;
+        c->h_frames[i].h = frames[i].height;
+        c->h_frames[i].stride = frames[i].row_stride;
     }
-    // pageable sources: HIP stages them before returning, so the vectors may die here
-    HIP_TRY(hipMemcpyAsync(c->views, vd.data(), nv * sizeof(zr::ViewDesc), hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipMemcpyAsync(c->frames, fd.data(), nf * sizeof(zr::FrameDesc), hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(c->views, c->h_views, nv * sizeof(zr::ViewDesc), hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(c->frames, c->h_frames, nf * sizeof(zr::FrameDesc), hipMemcpyHostToDevice, stream));
     return ZR_OK;
 }
 
@@ -601,10 +618,42 @@ int zr_free(void *p) {
     return ZR_OK;
 }
 
+int zr_host_alloc(void **p, size_t bytes) {
+    if (!p) return set_err(ZR_ERR_INVALID_ARGUMENT, "null p");
+    HIP_TRY(hipHostMalloc(p, bytes ? bytes : 4));
+    return ZR_OK;
+}
+
+int zr_host_free(void *p) {
+    HIP_TRY(hipHostFree(p));
+    return ZR_OK;
+}
+
 int zr_memcpy_async(void *dst, const void *src, size_t bytes, int kind, void *hip_stream) {
     hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost
                                                                     : hipMemcpyDeviceToDevice;
     HIP_TRY(hipMemcpyAsync(dst, src, bytes, k, (hipStream_t)hip_stream));
+    return ZR_OK;
+}
+
+int zr_event_create(void **event) {
+    if (!event) return set_err(ZR_ERR_INVALID_ARGUMENT, "null event");
+    HIP_TRY(hipEventCreateWithFlags((hipEvent_t *)event, hipEventDisableTiming));
+    return ZR_OK;
+}
+
+int zr_event_destroy(void *event) {
+    HIP_TRY(hipEventDestroy((hipEvent_t)event));
+    return ZR_OK;
+}
+
+int zr_event_record(void *event, void *stream) {
+    HIP_TRY(hipEventRecord((hipEvent_t)event, (hipStream_t)stream));
+    return ZR_OK;
+}
+
+int zr_event_synchronize(void *event) {
+    HIP_TRY(hipEventSynchronize((hipEvent_t)event));
     return ZR_OK;
 }
 
