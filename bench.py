@@ -10,9 +10,10 @@ exact host decode + weighted NMS, GPU ROI preprocessing + FaceMesh, host landmar
 ROI update.  With N > 1 every rank all-gathers its fixed-size detection records over RCCL
 (the single collective of SURVEY.md §8e) inside the timed region.
 
-Synthetic data: seeded uniform-noise frames carrying one synthetic face patch per frame
-(tools/make_face_patch.py) when available; frames whose detector finds nothing are tracked on a
-seeded square ROI ("forced-ROI mode") so every frame runs FaceMesh once.
+Synthetic data: seeded uniform-noise frames, each carrying one face patch (the reference's
+own FaceMesh test image, upscaled; see load_patch) at a seeded position; frames whose detector
+finds nothing are tracked on a seeded square ROI ("forced-ROI mode") so every
+frame runs FaceMesh at least once.
 
 Prints ONE JSON line (rank 0).  `--workload hand` runs config 4 (palm + 4 hand ROIs) instead.
 """
@@ -81,8 +82,15 @@ def forced_rois(rng, n, workload, h=1080, w=1920):
 
 
 def load_patch():
-    p = os.path.join(REPO, "tests", "golden", "face_patch.npy")
-    return np.load(p) if os.path.exists(p) else None
+    """A face to paste into the noise frames: the reference's own FaceMesh test image
+    (tests/golden/sad_linus_mesh.npz, the 192x192 colour codes of sad_linus_cropped.jpg),
+    upscaled 3x to 576x576, so the face spans ~400 px of the 1920-px frame and BlazeFace's
+    128-px letterbox sees it at ~27 px (the size its own test image has)."""
+    p = os.path.join(REPO, "tests", "golden", "sad_linus_mesh.npz")
+    codes = np.load(p)["codes"][0]  # [3, 192, 192] uint8
+    img = np.full((192, 192, 4), 255, np.uint8)
+    img[..., :3] = codes.transpose(1, 2, 0)
+    return np.repeat(np.repeat(img, 3, axis=0), 3, axis=1)
 
 
 # ---------------------------------------------------------------- CPU baseline (oracle)
@@ -278,7 +286,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic: seeded uniform-noise 1920x1080 RGBA8 frames"
-                + (" + one synthetic face patch each" if load_patch() is not None and args.workload == "face" else "")
+                + (" + one 576x576 face patch each (reference test image, upscaled)" if args.workload == "face" else "")
                 + "; forced seeded ROI when no detection; ONNX weights from the reference",
         "config": {"workload": "face pipeline BlazeFace->FaceMesh V1 (config 3/5)" if args.workload == "face"
                    else "palm lite + hand landmark lite, 4 ROIs/frame (config 4)",

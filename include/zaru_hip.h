@@ -137,6 +137,7 @@ int zr_event_create(void **event);
 int zr_event_destroy(void *event);
 int zr_event_record(void *event, void *stream);
 int zr_event_synchronize(void *event);
+int zr_event_query(void *event); /* ZR_OK when complete, 1 while pending */
 
 #ifdef __cplusplus
 }

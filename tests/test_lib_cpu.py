@@ -23,13 +23,13 @@ def test_library_exports_header_symbols():
 
 
 @pytest.mark.parametrize("model,launches", [
-    ("face_detection_short_range", 37), ("face_landmark", 45),
-    ("palm_detection_lite", 55), ("hand_landmark_lite", 52)])
+    ("face_detection_short_range", 21), ("face_landmark", 25),
+    ("palm_detection_lite", 32), ("hand_landmark_lite", 37)])
 def test_plan_compiles_and_fuses(models_dir, model, launches):
     data = open(os.path.join(models_dir, model + ".onnx"), "rb").read()
     txt = _lib.plan_describe(data)
     steps = [l for l in txt.splitlines() if l.split(" ")[0] in
-             ("gemm", "dw", "direct", "elt", "resize", "gap")]
+             ("gemm", "dw", "direct", "elt", "resize", "gap", "dwpw")]
     assert len(steps) == launches
     # no standalone element-wise pass survives: residual/pad/pool/act are all fused
     assert not [l for l in steps if l.startswith("elt")]

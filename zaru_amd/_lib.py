@@ -68,6 +68,7 @@ SIGNATURES = [
     ("zr_event_destroy", _I, [_P]),
     ("zr_event_record", _I, [_P, _P]),
     ("zr_event_synchronize", _I, [_P]),
+    ("zr_event_query", _I, [_P]),
 ]
 
 

@@ -6,6 +6,7 @@
 #include <pybind11/stl.h>
 
 #include "detection.h"
+#include "hand_tracker.h"
 #include "landmark.h"
 #include "pipeline.h"
 
@@ -149,12 +150,16 @@ PYBIND11_MODULE(_zaru_host, m) {
     m.def("candidate_logit_floor", &candidate_logit_floor);
 
     py::class_<Detection>(m, "Detection")
-        .def(py::init([](float conf, const Rect &r) {
+        .def(py::init([](float conf, const Rect &r, float angle,
+                         const std::vector<std::pair<float, float>> &kps) {
                  Detection d;
                  d.confidence = conf;
                  d.rect = r;
+                 d.angle = angle;
+                 for (auto &k : kps) d.keypoints.push_back({k.first, k.second});
                  return d;
-             }), py::arg("confidence"), py::arg("rect"))
+             }), py::arg("confidence"), py::arg("rect"), py::arg("angle") = 0.f,
+             py::arg("keypoints") = std::vector<std::pair<float, float>>{})
         .def("confidence", [](const Detection &d) { return d.confidence; })
         .def("angle", [](const Detection &d) { return d.angle; })
         .def("bounding_rect", [](const Detection &d) { return d.rect; })
@@ -185,6 +190,12 @@ PYBIND11_MODULE(_zaru_host, m) {
         return o;
     });
     m.def("set_models_dir", &set_models_dir);
+    m.def("pack_detection_records", [](const std::vector<std::vector<Detection>> &dets,
+                                       const std::vector<uint32_t> &frame_ids, uint32_t rmax) {
+        py::array_t<float> a({(py::ssize_t)dets.size(), (py::ssize_t)det_record_width(rmax)});
+        pack_detection_records(dets, frame_ids, rmax, a.mutable_data());
+        return a;
+    }, py::arg("detections"), py::arg("frame_ids"), py::arg("rmax") = 8);
 
     py::class_<Detector>(m, "Detector")
         .def(py::init([](const std::string &net, int device) { return new Detector(detector_net(net), device); }),
@@ -235,6 +246,33 @@ PYBIND11_MODULE(_zaru_host, m) {
             d["updated_roi"] = r->updated_roi;
             return d;
         });
+
+    py::class_<HandTracker>(m, "HandTracker")
+        .def(py::init<int>(), py::arg("device") = 0)
+        .def("set_redetect_interval", &HandTracker::set_redetect_interval, py::arg("ms"))
+        .def("set_iou_thresh", &HandTracker::set_iou_thresh)
+        .def("set_loss_threshold", &HandTracker::set_loss_threshold)
+        .def("track", [](HandTracker &t, py::array_t<uint8_t, py::array::c_style> img, py::object now_ms) {
+                 Image im = host_image(img);
+                 if (now_ms.is_none()) t.track(im);
+                 else t.track(im, now_ms.cast<double>());
+             }, py::arg("image"), py::arg("now_ms") = py::none())
+        .def("hands", [](const HandTracker &t) {
+            py::list out;
+            for (const auto &h : t.hands()) {
+                py::dict d = estimate_dict(h.landmarks);
+                d["id"] = h.id;
+                d["view_rect"] = h.view_rect;
+                out.append(d);
+            }
+            return out;
+        })
+        .def("wait_detection", &HandTracker::wait_detection)
+        .def("inject_detections", &HandTracker::inject_detections)
+        .def("detection_running", &HandTracker::detection_running)
+        .def("num_tracked", &HandTracker::num_tracked)
+        .def_static("filter_detections", &HandTracker::filter_detections)
+        .def_static("dedupe_rois", &HandTracker::dedupe_rois);
 
     py::class_<DetectTrackPipeline>(m, "DetectTrackPipeline")
         .def(py::init([](const std::string &kind, int device, int threads, uint32_t max_rois,
@@ -294,6 +332,15 @@ PYBIND11_MODULE(_zaru_host, m) {
             return p.rois().size();
         })
         .def("detections", [](const DetectTrackPipeline &p) { return p.detections(); })
+        .def("detection_records", [](const DetectTrackPipeline &p, uint32_t rmax, uint32_t first_id,
+                                     uint32_t id_stride) {
+            const auto &d = p.detections();
+            std::vector<uint32_t> ids(d.size());
+            for (size_t i = 0; i < d.size(); i++) ids[i] = first_id + (uint32_t)i * id_stride;
+            py::array_t<float> a({(py::ssize_t)d.size(), (py::ssize_t)det_record_width(rmax)});
+            pack_detection_records(d, ids, rmax, a.mutable_data());
+            return a;
+        }, py::arg("rmax") = 8, py::arg("first_id") = 0, py::arg("id_stride") = 1)
         .def("num_rois", [](const DetectTrackPipeline &p) { return p.rois().size(); })
         .def("roi", [](const DetectTrackPipeline &p, size_t i) {
             const RoiResult &r = p.rois().at(i);

@@ -155,6 +155,33 @@ void map_detections(std::vector<Detection> &dets, const Rect &rect, uint32_t in_
     }
 }
 
+void pack_detection_records(const std::vector<std::vector<Detection>> &dets,
+                            const std::vector<uint32_t> &frame_ids, uint32_t rmax, float *out) {
+    const uint32_t w = det_record_width(rmax);
+    for (size_t f = 0; f < dets.size(); f++) {
+        float *r = out + f * w;
+        std::fill(r, r + w, 0.f);
+        const uint32_t id = f < frame_ids.size() ? frame_ids[f] : (uint32_t)f;
+        const uint32_t cnt = (uint32_t)dets[f].size();
+        std::memcpy(&r[0], &id, 4);
+        std::memcpy(&r[1], &cnt, 4);
+        for (uint32_t k = 0; k < std::min<uint32_t>(cnt, rmax); k++) {
+            const Detection &d = dets[f][k];
+            float *e = r + 2 + DET_RECORD_FIELDS * k;
+            e[0] = d.confidence;
+            e[1] = d.angle;
+            e[2] = d.rect.center().x;
+            e[3] = d.rect.center().y;
+            e[4] = d.rect.width();
+            e[5] = d.rect.height();
+            for (size_t p = 0; p < d.keypoints.size() && p < 7; p++) {
+                e[6 + 2 * p] = d.keypoints[p].x;
+                e[7 + 2 * p] = d.keypoints[p].y;
+            }
+        }
+    }
+}
+
 ViewData letterbox_view(uint32_t w, uint32_t h, AspectRatio in_aspect, Rect *rect_out) {
     const ViewData full = ViewData::full(w, h);
     const Rect rect = full.local_rect().grow_to_fit_aspect(in_aspect);

@@ -66,6 +66,14 @@ struct DetectorNetwork {
 // Detector::detect_impl steps after inference (detection.rs:245-267)
 void map_detections(std::vector<Detection> &dets, const Rect &letterbox, uint32_t in_w);
 
+// Fixed-size detection records, the payload of the multi-GPU all-gather: per
+// frame {frame id (u32 bits), count (u32 bits)} then `rmax` x {conf, angle, cx, cy, w, h,
+// 7 x (kx, ky)} (20 f32 each, zero-padded; detections beyond rmax are dropped, count is not).
+constexpr uint32_t DET_RECORD_FIELDS = 20;
+inline uint32_t det_record_width(uint32_t rmax) { return 2 + DET_RECORD_FIELDS * rmax; }
+void pack_detection_records(const std::vector<std::vector<Detection>> &dets,
+                            const std::vector<uint32_t> &frame_ids, uint32_t rmax, float *out);
+
 class Detector {  // detection.rs:152-276
   public:
     static constexpr float DEFAULT_THRESHOLD = 0.5f;

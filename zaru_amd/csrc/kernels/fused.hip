@@ -1,0 +1,303 @@
+// fused.hip -- the two kernels that cut the plan's HBM traffic the most:
+//   * stem_kernel: the dense KxK stride-S stem conv (Cin = 3, the first layer of all four
+//     models) with every output channel of a pixel in registers and the weights read through
+//     the scalar cache.  With PRE it samples its input straight from the RGBA frames through
+//     the per-image views (K1 fused in front), so the f32 input tensor never exists.
+//   * dwpw_kernel: a depthwise KxK conv feeding a 1x1 conv (the BlazeBlock / inverted-residual
+//     tail) in one launch; the depthwise output of a column tile lives only in LDS.
+// Reference: the Conv nodes of the four ONNX graphs that ORT/tract execute at
+// crates/zaru/src/nn/mod.rs:483-533, and the image->tensor map at nn/mod.rs:54-73.
+#include <cstdio>
+
+#include "../runtime/zr_kernels.h"
+#include "act.h"
+#include "epilogue.h"
+#include "sample.h"
+
+namespace zr {
+
+// ------------------------------------------------------------------ stem
+constexpr int STH = 8, STW = 32;  // output tile: 8 rows x 32 columns, one pixel per thread
+
+template <int K, int S, int CO, bool PRE>
+__global__ __launch_bounds__(256) void stem_kernel(const StemParams P) {
+    constexpr int RIN = (STH - 1) * S + K, WIN = (STW - 1) * S + K;
+    __shared__ float patch[3][RIN][WIN];
+    const int tiles_x = (P.OW + STW - 1) / STW;
+    const int ty0 = (blockIdx.x / tiles_x) * STH, tx0 = (blockIdx.x % tiles_x) * STW;
+    const int n = blockIdx.y;
+    const int iy0 = ty0 * S - P.pad_t, ix0 = tx0 * S - P.pad_l;
+    if constexpr (PRE) {
+        // all of this thread's pixel gathers are issued before the first is used
+        constexpr int NP = (RIN * WIN + 255) / 256;
+        const ViewDesc d = P.pre.views[n];
+        const FrameDesc f = P.pre.frames[d.frame];
+        uint32_t px[NP];
+        bool pad[NP];
+#pragma unroll
+        for (int u = 0; u < NP; ++u) {
+            const int i = threadIdx.x + 256 * u;
+            const int r = i / WIN, x = i - r * WIN;
+            const int iy = iy0 + r, ix = ix0 + x;
+            // outside the network input: the ONNX zero padding of the f32 tensor
+            pad[u] = !(i < RIN * WIN && iy >= 0 && iy < P.IH && ix >= 0 && ix < P.IW);
+            px[u] = load_pixel(f, pad[u] ? -1 : sample_offset(d, f, ix, iy, P.IW, P.IH));
+        }
+#pragma unroll
+        for (int u = 0; u < NP; ++u) {
+            const int i = threadIdx.x + 256 * u;
+            if (i >= RIN * WIN) break;
+            const int r = i / WIN, x = i - r * WIN;
+            patch[0][r][x] = pad[u] ? 0.f : color_map(px[u], 0, P.pre.adjust, P.pre.lo);
+            patch[1][r][x] = pad[u] ? 0.f : color_map(px[u], 1, P.pre.adjust, P.pre.lo);
+            patch[2][r][x] = pad[u] ? 0.f : color_map(px[u], 2, P.pre.adjust, P.pre.lo);
+        }
+    } else {
+        const float *src = P.in.p + (int64_t)n * P.in.sN;
+        for (int i = threadIdx.x; i < 3 * RIN * WIN; i += 256) {
+            const int c = i / (RIN * WIN), rem = i - c * (RIN * WIN);
+            const int r = rem / WIN, x = rem - r * WIN;
+            const int iy = iy0 + r, ix = ix0 + x;
+            (&patch[0][0][0])[i] = (iy >= 0 && iy < P.IH && ix >= 0 && ix < P.IW)
+                                       ? src[(int64_t)c * P.in.sC + (int64_t)iy * P.IW + ix]
+                                       : 0.f;
+        }
+    }
+    __syncthreads();
+    const int ly = threadIdx.x / STW, lx = threadIdx.x - ly * STW;
+    float acc[CO];
+#pragma unroll
+    for (int o = 0; o < CO; ++o) acc[o] = 0.f;
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < K; ++kx) {
+                const float v = patch[c][ly * S + ky][lx * S + kx];
+                const float *w = P.w + (c * K + ky) * K + kx;  // uniform: scalar loads
+#pragma unroll
+                for (int o = 0; o < CO; ++o) acc[o] = __builtin_fmaf(w[o * 3 * K * K], v, acc[o]);
+            }
+    const int oy = ty0 + ly, ox = tx0 + lx;
+    if (oy >= P.OH || ox >= P.OW) return;
+    float *dst = P.out + (int64_t)n * P.o_sN + (int64_t)oy * P.OW + ox;
+#pragma unroll
+    for (int o = 0; o < CO; ++o)
+        if (o < P.Cout) dst[(int64_t)o * P.o_sC] = apply_act(P.act, acc[o] + P.bias[o], o);
+}
+
+bool stem_supported(int cin, int k, int stride, int cout) {
+    return cin == 3 && (k == 3 || k == 5) && (stride == 1 || stride == 2) && cout >= 1 && cout <= 32;
+}
+
+template <int K, int S, int CO>
+static const char *stem_go(const StemParams &p, bool pre, hipStream_t s) {
+    const int tiles = ((p.OH + STH - 1) / STH) * ((p.OW + STW - 1) / STW);
+    dim3 grid(tiles, p.N);
+    if (pre) hipLaunchKernelGGL((stem_kernel<K, S, CO, true>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((stem_kernel<K, S, CO, false>), grid, dim3(256), 0, s, p);
+    return pre ? "stem_kernel<pre>" : "stem_kernel";
+}
+
+template <int K, int S>
+static const char *stem_co(const StemParams &p, bool pre, hipStream_t s) {
+    if (p.Cout <= 16) return stem_go<K, S, 16>(p, pre, s);
+    if (p.Cout <= 24) return stem_go<K, S, 24>(p, pre, s);
+    return stem_go<K, S, 32>(p, pre, s);
+}
+
+const char *launch_stem(const StemParams &p, bool pre, hipStream_t s) {
+    if (p.k == 3) return p.stride == 1 ? stem_co<3, 1>(p, pre, s) : stem_co<3, 2>(p, pre, s);
+    return p.stride == 1 ? stem_co<5, 1>(p, pre, s) : stem_co<5, 2>(p, pre, s);
+}
+
+// ------------------------------------------------------------------ depthwise -> 1x1
+// A workgroup (4 waves) owns a BM x BN output tile: BN consecutive columns j = n*P + q of the
+// 1x1 conv's output and BM of its output channels.  The waves are laid out WM along M and
+// 4/WM along N; each wave holds MTW x NTW 32x32 accumulator tiles.  Per chunk of FKC input
+// channels:
+//   1. the workgroup computes the depthwise outputs of the chunk for its BN columns into LDS
+//      (taps straight from L1/L2, where neighbouring columns share them; every tap of the
+//      chunk is issued before the first is used; clamped addresses + a validity mask, never a
+//      branch around a load);
+//   2. the chunk of the transposed 1x1 weights goes to LDS;
+//   3. every wave runs v_mfma_f32_32x32x2_f32 over the chunk.
+// The epilogue is epilogue_tile: bias, activation, residual (+pad/+pool), activation.
+// The layout is chosen per layer (launch_dwpw) so that a launch has enough workgroups to fill
+// 256 CUs without splitting M (which would recompute the depthwise part): wide column tiles
+// for the few-channel high-resolution layers, tall channel tiles for the 128/256-channel
+// low-resolution ones.  Column tiles are dealt to XCDs in contiguous runs, so halo rows and the
+// residual re-read are L2 hits on the XCD that just fetched them.
+template <int K, int S, int WM, int MTW, int NTW>
+__global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) {
+    constexpr int WN = 4 / WM;
+    constexpr int BN = WN * NTW * 32, BM = WM * MTW * 32;
+    constexpr int KK = K * K;
+    constexpr int FKC = K == 3 ? 16 : 8;  // input channels per chunk
+    constexpr int CPAR = 256 / BN;        // channels whose depthwise runs side by side
+    constexpr int PER = FKC / CPAR;       // depthwise outputs per thread per chunk
+    static_assert(PER >= 1 && FKC % CPAR == 0, "tile/chunk mismatch");
+    __shared__ float sD[FKC][BN];
+    __shared__ float sW[FKC][BM];
+    const GemmParams &G = P.g;
+
+    const int cpx = gridDim.x >> 3;  // gridDim.x is a multiple of 8
+    const int tile = (blockIdx.x & 7) * cpx + (blockIdx.x >> 3);
+    if (tile >= nct) return;  // whole workgroup, before any barrier
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kh = lane >> 5, col = lane & 31;
+    const int wm = wave % WM, wn = wave / WM;
+    const int j0 = tile * BN, m0 = blockIdx.y * BM;
+    const int Cin = G.K;
+
+    // depthwise role: column dj of the tile, channels dc, dc + CPAR, ... of each chunk
+    const int dj = tid % BN;
+    int dc = tid / BN;
+    if constexpr (BN >= 64) dc = __builtin_amdgcn_readfirstlane(dc);  // one channel per wave
+    const int jd = min(j0 + dj, G.ncols - 1);
+    const int n = jd / G.P, q = jd - n * G.P;
+    const int oy = q / P.OW, ox = q - oy * P.OW;
+    const int iy0 = oy * S - P.pad_t, ix0 = ox * S - P.pad_l;
+    const int H = P.in.H, W = P.in.W;
+    int off[KK];
+    uint32_t mask = 0;
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) {
+            const int iy = iy0 + ky, ix = ix0 + kx;
+            const bool ok = iy >= 0 && iy < H && ix >= 0 && ix < W;
+            off[ky * K + kx] = ok ? iy * W + ix : 0;
+            mask |= (ok ? 1u : 0u) << (ky * K + kx);
+        }
+    const float *src = P.in.p + (int64_t)n * P.in.sN;
+
+    f32x16 acc[MTW][NTW];
+#pragma unroll
+    for (int t = 0; t < MTW; ++t)
+#pragma unroll
+        for (int u = 0; u < NTW; ++u)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
+
+    for (int kc = 0; kc < Cin; kc += FKC) {
+        float tap[PER][KK];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int c = kc + dc + CPAR * i;
+            const float *pl = src + (int64_t)(c < Cin ? c : Cin - 1) * P.in.sC;
+#pragma unroll
+            for (int t = 0; t < KK; ++t) tap[i][t] = pl[off[t]];
+        }
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int c = kc + dc + CPAR * i;
+            const int cl = c < Cin ? c : Cin - 1;
+            const float *w = P.dw_w + cl * KK;
+            float a = P.dw_b[cl];
+#pragma unroll
+            for (int t = 0; t < KK; ++t) a = __builtin_fmaf(w[t], ((mask >> t) & 1u) ? tap[i][t] : 0.f, a);
+            a = apply_act(P.dw_act, a, cl);
+            sD[dc + CPAR * i][dj] = c < Cin ? a : 0.f;
+        }
+        for (int i = tid; i < FKC * BM; i += 256) {
+            const int r = i / BM, cc = i - r * BM;
+            const int k = kc + r, m = m0 + cc;
+            sW[r][cc] = (k < Cin && m < G.Mpad) ? G.wt[(int64_t)k * G.Mpad + m] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < FKC / 2; ++s) {
+            float a[MTW], b[NTW];
+#pragma unroll
+            for (int t = 0; t < MTW; ++t) a[t] = sW[2 * s + kh][(wm * MTW + t) * 32 + col];
+#pragma unroll
+            for (int u = 0; u < NTW; ++u) b[u] = sD[2 * s + kh][(wn * NTW + u) * 32 + col];
+#pragma unroll
+            for (int t = 0; t < MTW; ++t)
+#pragma unroll
+                for (int u = 0; u < NTW; ++u)
+                    acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t], b[u], acc[t][u], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+
+#pragma unroll
+    for (int u = 0; u < NTW; ++u) {
+        const int j = j0 + (wn * NTW + u) * 32 + col;
+        if (j >= G.ncols) continue;
+        const int on = j / G.P, oq = j - on * G.P;
+#pragma unroll
+        for (int t = 0; t < MTW; ++t) epilogue_tile(G, acc[t][u], on, oq, m0 + (wm * MTW + t) * 32, kh);
+    }
+}
+
+bool dwpw_supported(int k, int stride) { return (k == 3 || k == 5) && (stride == 1 || stride == 2); }
+
+namespace {
+
+struct DwPwLayout {
+    int wm, mtw, ntw;
+    int bm() const { return wm * mtw * 32; }
+    int bn() const { return (4 / wm) * ntw * 32; }
+};
+// the instantiated layouts (BM x BN): 32x128 64x128 96x128 128x128 | 64x64 128x64 256x64 |
+// 128x32 256x32
+constexpr DwPwLayout kLayouts[] = {{1, 1, 1}, {1, 2, 1}, {1, 3, 1}, {1, 4, 1}, {2, 1, 1},
+                                   {2, 2, 1}, {2, 4, 1}, {4, 1, 1}, {4, 2, 1}};
+
+template <int K, int S, int WM, int MTW>
+const char *dwpw_go(const DwPwParams &p, hipStream_t s) {
+    constexpr int BN = (4 / WM) * 32, BM = WM * MTW * 32;
+    const int nct = (p.g.ncols + BN - 1) / BN;
+    const int mb = (p.g.Mpad + BM - 1) / BM;
+    dim3 grid((nct + 7) / 8 * 8, mb);
+    hipLaunchKernelGGL((dwpw_kernel<K, S, WM, MTW, 1>), grid, dim3(256), 0, s, p, nct);
+    static char names[2][2][5][5][40];
+    char *nm = names[K == 5][S == 2][WM][MTW];
+    if (!nm[0]) snprintf(nm, 40, "dwpw_kernel<%d,%d,%dx%d>", K, S, BM, BN);
+    return nm;
+}
+
+template <int K, int S>
+const char *dwpw_layout(const DwPwParams &p, const DwPwLayout &l, hipStream_t s) {
+    switch (l.wm * 10 + l.mtw) {
+    case 11: return dwpw_go<K, S, 1, 1>(p, s);
+    case 12: return dwpw_go<K, S, 1, 2>(p, s);
+    case 13: return dwpw_go<K, S, 1, 3>(p, s);
+    case 14: return dwpw_go<K, S, 1, 4>(p, s);
+    case 21: return dwpw_go<K, S, 2, 1>(p, s);
+    case 22: return dwpw_go<K, S, 2, 2>(p, s);
+    case 24: return dwpw_go<K, S, 2, 4>(p, s);
+    case 41: return dwpw_go<K, S, 4, 1>(p, s);
+    default: return dwpw_go<K, S, 4, 2>(p, s);
+    }
+}
+
+}  // namespace
+
+// Layout choice: no M split unless Mpad > 256, at most 1/3 padded rows; among those, the
+// widest column tile that still gives >= 4 workgroups per CU (else the most workgroups).
+const char *launch_dwpw(const DwPwParams &p, hipStream_t s) {
+    const DwPwLayout *best = nullptr;
+    int64_t best_wgs = 0;
+    for (const DwPwLayout &l : kLayouts) {
+        const int mb = (p.g.Mpad + l.bm() - 1) / l.bm();
+        if (mb > 1 && l.bm() < 256) continue;
+        if ((int64_t)mb * l.bm() * 3 > (int64_t)p.g.Mpad * 4 && p.g.Mpad <= 256) continue;
+        const int64_t wgs = (int64_t)((p.g.ncols + l.bn() - 1) / l.bn()) * mb;
+        bool better;
+        if (!best) better = true;
+        else if ((wgs >= 1024) != (best_wgs >= 1024)) better = wgs >= 1024;
+        else if (wgs >= 1024) better = l.bn() > best->bn() || (l.bn() == best->bn() && l.bm() < best->bm());
+        else better = wgs > best_wgs || (wgs == best_wgs && l.bm() < best->bm());
+        if (better) {
+            best = &l;
+            best_wgs = wgs;
+        }
+    }
+    if (p.k == 3) return p.stride == 1 ? dwpw_layout<3, 1>(p, *best, s) : dwpw_layout<3, 2>(p, *best, s);
+    return p.stride == 1 ? dwpw_layout<5, 1>(p, *best, s) : dwpw_layout<5, 2>(p, *best, s);
+}
+
+}  // namespace zr

@@ -15,10 +15,9 @@
 // crates/zaru/src/nn/mod.rs:483-533.
 #include "../runtime/zr_kernels.h"
 #include "act.h"
+#include "epilogue.h"
 
 namespace zr {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int KC = 32;  // K rows per LDS stage
 
@@ -73,29 +72,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmParams P) {
     }
 
     if (!valid) return;
-    // C/D map of 32x32 MFMA: column = lane%32, row = (r&3) + 8*(r>>2) + 4*(lane/32)
-    float *ob = P.out + (int64_t)n * P.o_sN + (int64_t)q * P.o_sP;
 #pragma unroll
-    for (int t = 0; t < MT; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int m = m0 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-            if (m >= P.M) continue;
-            float v = apply_act(P.pre, acc[t][r] + P.bias[m], m);
-            if (P.res_mode != 0 && m < P.r_C) {
-                const float *rb = P.r + (int64_t)n * P.r_sN + (int64_t)m * P.r_sC;
-                float rv;
-                if (P.res_mode == 1) {
-                    rv = rb[q];
-                } else {
-                    const int y = q / P.out_W, x = q - y * P.out_W;
-                    const float *s0 = rb + (int64_t)(2 * y) * P.r_W + 2 * x;
-                    rv = fmaxf(fmaxf(s0[0], s0[1]), fmaxf(s0[P.r_W], s0[P.r_W + 1]));
-                }
-                v += rv;
-            }
-            ob[(int64_t)m * P.o_sC] = apply_act(P.post, v, m);
-        }
+    for (int t = 0; t < MT; ++t) epilogue_tile(P, acc[t], n, q, m0 + t * 32, kh);
 }
 
 // ---------------------------------------------------------------- LDS-tiled variant
@@ -199,28 +177,8 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const GemmParams P, int
         const int j = j0 + (wave * NT + u) * 32 + col;
         if (j >= P.ncols) continue;
         const int n = j / P.P, q = j - n * P.P;
-        float *ob = P.out + (int64_t)n * P.o_sN + (int64_t)q * P.o_sP;
 #pragma unroll
-        for (int t = 0; t < MT; ++t)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = m0 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-                if (m >= P.M) continue;
-                float v = apply_act(P.pre, acc[t][u][r] + P.bias[m], m);
-                if (P.res_mode != 0 && m < P.r_C) {
-                    const float *rb = P.r + (int64_t)n * P.r_sN + (int64_t)m * P.r_sC;
-                    float rv;
-                    if (P.res_mode == 1) {
-                        rv = rb[q];
-                    } else {
-                        const int y = q / P.out_W, x = q - y * P.out_W;
-                        const float *s0 = rb + (int64_t)(2 * y) * P.r_W + 2 * x;
-                        rv = fmaxf(fmaxf(s0[0], s0[1]), fmaxf(s0[P.r_W], s0[P.r_W + 1]));
-                    }
-                    v += rv;
-                }
-                ob[(int64_t)m * P.o_sC] = apply_act(P.post, v, m);
-            }
+        for (int t = 0; t < MT; ++t) epilogue_tile(P, acc[t][u], n, q, m0 + t * 32, kh);
     }
 }
 

@@ -370,6 +370,7 @@ bool Compiler::lower_conv(const OnnxNode &nd) {
         s.b_off = push_weights(bias);
     } else if (pointwise || fullplane) {
         s.kind = S_GEMM;
+        s.in2 = TRef{};
         s.KK = kh * kw;
         s.M = Mo;
         s.K = Cin * s.KK;
@@ -384,10 +385,42 @@ bool Compiler::lower_conv(const OnnxNode &nd) {
     } else if (g == 1 && st[0] == st[1]) {
         s.kind = S_DIRECT;
         s.M = Mo;
-        s.w_off = push_weights(w->f);
+        s.stem = kh == kw && stem_supported(Cin, kh, (int)st[0], Mo);
+        std::vector<float> wf = w->f;
+        if (s.stem) {  // stem_kernel reads 32 output channels of weights unconditionally
+            wf.resize((size_t)32 * Cin * kh * kw, 0.f);
+            bias.resize(32, 0.f);
+        }
+        s.w_off = push_weights(wf);
         s.b_off = push_weights(bias);
+        s.bytes_pre = 4.0 * ((double)H * W + (double)Mo * OH * OW);
     } else {
         return fail("Conv " + s.name + ": unsupported configuration");
+    }
+    // A 1x1 conv whose input is a depthwise conv's private output (the step just lowered)
+    // absorbs it: the depthwise result then never leaves the CU (fused.hip dwpw_kernel).
+    if (pointwise && !P.steps.empty()) {
+        Val &xv = val(xn);
+        const Step &d = P.steps.back();
+        if (xv.step == (int)P.steps.size() - 1 && xv.consumers == 1 && xv.out_idx < 0 &&
+            d.kind == S_DW && d.out.kind == 0 && dwpw_supported(d.kh, d.stride)) {
+            Step f = s;
+            f.kind = S_DWPW;
+            f.in = d.in;
+            f.kh = d.kh;
+            f.kw = d.kw;
+            f.stride = d.stride;
+            f.pad_t = d.pad_t;
+            f.pad_l = d.pad_l;
+            f.dw_w_off = d.w_off;
+            f.dw_b_off = d.b_off;
+            f.dw_act = d.pre;
+            f.flops = d.flops + s.flops;
+            // depthwise input read + 1x1 output write; the intermediate is on chip
+            f.bytes = 4.0 * ((double)d.in.C * d.in.H * d.in.W + (double)Mo * OH * OW);
+            P.steps.pop_back();
+            s = f;
+        }
     }
     s.out = out_ref(nd.out[0], Mo, OH, OW);
     P.steps.push_back(s);
@@ -442,11 +475,12 @@ bool Compiler::lower_act(const OnnxNode &nd) {
     if (x.step >= 0 && x.consumers == 1 && x.out_idx < 0) {
         Step &s = P.steps[x.step];
         ActDesc a;
-        const int Cpad = s.kind == S_GEMM ? s.Mpad : C;
+        const bool gemm = s.kind == S_GEMM || s.kind == S_DWPW;
+        const int Cpad = gemm ? s.Mpad : (s.stem ? std::max(C, 32) : C);
         ActDesc *slot = nullptr;
-        if (s.kind == S_GEMM) slot = s.res_mode ? &s.post : (s.pre.kind ? nullptr : &s.pre);
+        if (gemm) slot = s.res_mode ? &s.post : (s.pre.kind ? nullptr : &s.pre);
         else if (s.kind == S_DW || s.kind == S_DIRECT || s.kind == S_ELT) slot = s.pre.kind ? nullptr : &s.pre;
-        if (s.kind == S_GEMM && s.res_mode && s.post.kind) slot = nullptr;
+        if (gemm && s.res_mode && s.post.kind) slot = nullptr;
         if (slot) {
             if (!act_from_node(nd, C, Cpad, a)) return false;
             *slot = a;
@@ -486,7 +520,9 @@ bool Compiler::lower_add(const OnnxNode &nd) {
         Val &p = val(pn);
         if (p.step < 0 || p.consumers != 1 || p.out_idx >= 0) continue;
         const int si = p.step;
-        if (P.steps[si].kind != S_GEMM || P.steps[si].res_mode || P.steps[si].post.kind) continue;
+        if ((P.steps[si].kind != S_GEMM && P.steps[si].kind != S_DWPW) || P.steps[si].res_mode ||
+            P.steps[si].post.kind)
+            continue;
         // resolve the shortcut through lazily kept Pad / MaxPool nodes
         std::string r = rn;
         int rc = (int)val(r).shape[1];
@@ -719,6 +755,14 @@ bool Compiler::run(const std::vector<uint32_t> &sel) {
         P.flops_per_image += s.flops;
     }
     P.bytes_per_image += 0;  // input read is counted by the stem
+    int readers = 0, reader = -1;
+    for (size_t i = 0; i < P.steps.size(); i++)
+        for (const TRef *r : {&P.steps[i].in, &P.steps[i].in2})
+            if (r->kind == 1) {
+                readers++;
+                reader = (int)i;
+            }
+    P.input_fusable = readers == 1 && P.steps[reader].kind == S_DIRECT && P.steps[reader].stem;
     allocate();
     return true;
 }
@@ -826,6 +870,46 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook
             kname = launch_gemm(g, stream);
             break;
         }
+        case S_DWPW: {
+            DwPwParams d{};
+            GemmParams &g = d.g;
+            g.P = s.out.H * s.out.W;
+            g.ncols = b.N * g.P;
+            g.M = s.M;
+            g.K = s.K;
+            g.KK = 1;
+            g.Mpad = s.Mpad;
+            g.Kpad = s.Kpad;
+            g.wt = W + s.w_off;
+            g.bias = W + s.b_off;
+            g.pre = act_of(s.pre, W);
+            g.post = act_of(s.post, W);
+            g.res_mode = s.res_mode;
+            if (s.res_mode) {
+                Resolved r = resolve(s.in2, plan, b);
+                g.r = r.p;
+                g.r_sN = r.sN;
+                g.r_sC = r.sC;
+                g.r_C = s.r_C;
+                g.r_W = s.in2.W;
+            }
+            g.out_W = s.out.W;
+            g.out = const_cast<float *>(out.p);
+            g.o_sN = out.sN;
+            g.o_sC = out.sC;
+            g.o_sP = out.sP;
+            d.in = plane_of(s.in, plan, b);
+            d.OW = s.out.W;
+            d.k = s.kh;
+            d.stride = s.stride;
+            d.pad_t = s.pad_t;
+            d.pad_l = s.pad_l;
+            d.dw_w = W + s.dw_w_off;
+            d.dw_b = W + s.dw_b_off;
+            d.dw_act = act_of(s.dw_act, W);
+            kname = launch_dwpw(d, stream);
+            break;
+        }
         case S_DW: {
             DwParams d{};
             d.in = plane_of(s.in, plan, b);
@@ -846,6 +930,31 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook
             break;
         }
         case S_DIRECT: {
+            if (s.stem) {
+                StemParams sp{};
+                const bool pre = s.in.kind == 1 && b.pre;
+                if (pre) sp.pre = *b.pre;
+                else sp.in = plane_of(s.in, plan, b);
+                sp.out = const_cast<float *>(out.p);
+                sp.o_sN = out.sN;
+                sp.o_sC = out.sC;
+                sp.IH = s.in.H;
+                sp.IW = s.in.W;
+                sp.OH = s.out.H;
+                sp.OW = s.out.W;
+                sp.N = b.N;
+                sp.Cout = s.M;
+                sp.k = s.kh;
+                sp.stride = s.stride;
+                sp.pad_t = s.pad_t;
+                sp.pad_l = s.pad_l;
+                sp.w = W + s.w_off;
+                sp.bias = W + s.b_off;
+                sp.act = act_of(s.pre, W);
+                kname = launch_stem(sp, pre, stream);
+                if (hook) hook->after(stream, kname, (pre ? s.bytes_pre : s.bytes) * b.N, s.flops * b.N);
+                continue;
+            }
             DirectParams d{};
             d.in = plane_of(s.in, plan, b);
             d.out = const_cast<float *>(out.p);

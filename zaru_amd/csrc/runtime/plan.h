@@ -18,7 +18,7 @@
 
 namespace zr {
 
-enum StepKind { S_GEMM, S_DW, S_DIRECT, S_ELT, S_RESIZE, S_GAP };
+enum StepKind { S_GEMM, S_DW, S_DIRECT, S_ELT, S_RESIZE, S_GAP, S_DWPW };
 
 struct TRef {
     int kind = 0;  // 0 internal storage, 1 graph input, 2 graph output
@@ -45,8 +45,14 @@ struct Step {
     int res_mode = 0, r_C = 0;
     int elt_op = 0;
     float scale_y = 1.f, scale_x = 1.f;
-    // algorithmic traffic / work per image (for roofline accounting)
-    double bytes = 0, flops = 0;
+    // S_DWPW: the depthwise conv in front of the 1x1 (kh/kw/stride/pads above describe it)
+    int64_t dw_w_off = -1, dw_b_off = -1;
+    ActDesc dw_act;
+    // S_DIRECT: runs as stem_kernel (Cin = 3, weights padded to 32 output channels)
+    bool stem = false;
+    // algorithmic traffic / work per image (for roofline accounting); bytes_pre: the same
+    // step sampling its input from RGBA frames (4 B per input pixel instead of 12)
+    double bytes = 0, flops = 0, bytes_pre = 0;
 };
 
 struct PlanOutput {
@@ -65,6 +71,8 @@ struct Plan {
     int in_C = 0, in_H = 0, in_W = 0;
     std::vector<PlanOutput> outputs;
     double bytes_per_image = 0, flops_per_image = 0;
+    // the graph input is read by exactly one step, a stem: view sampling can be fused into it
+    bool input_fusable = false;
 };
 
 bool compile_plan(const OnnxModel &m, const std::vector<uint32_t> &out_sel, Plan &plan,
@@ -77,6 +85,8 @@ struct Binding {
     float *const *outputs = nullptr;  // device pointers, one per plan output
     float *arena = nullptr;
     const float *weights = nullptr;
+    // when set, the input comes from RGBA frames through these views (plan.input_fusable)
+    const PreprocParams *pre = nullptr;
 };
 
 // Optional per-launch hook (profiling): called before and after every kernel launch with the

@@ -201,7 +201,7 @@ struct CtxLock {
 
 // enqueue the plan on `stream` with a context's workspace
 int enqueue(zr_session *s, Ctx *c, int N, const float *input, int64_t in_sN, int64_t in_sC,
-            float *const *outs, hipStream_t stream) {
+            float *const *outs, hipStream_t stream, const zr::PreprocParams *pre = nullptr) {
     const size_t need = (size_t)s->plan.arena_per_image * (size_t)N;
     if (int rc = grow(c->arena, c->arena_floats, need ? need : 1)) return rc;
     HIP_TRY(hipStreamWaitEvent(stream, c->done, 0));
@@ -213,6 +213,7 @@ int enqueue(zr_session *s, Ctx *c, int N, const float *input, int64_t in_sN, int
     b.outputs = outs;
     b.arena = c->arena;
     b.weights = s->weights;
+    b.pre = pre;
     {
         std::unique_lock<std::mutex> pl(s->prof.mu, std::defer_lock);
         if (s->prof.on) pl.lock();
@@ -257,6 +258,8 @@ int upload_views(Ctx *c, const zr_frame *frames, size_t nf, const zr_view *views
         c->h_views[i] = make_view(views[i], f);
     }
     for (size_t i = 0; i < nf; i++) {
+        if (!frames[i].rgba || frames[i].width == 0 || frames[i].height == 0)
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "empty frame");
         c->h_frames[i].rgba = frames[i].rgba;
         c->h_frames[i].w = frames[i].width;
         c->h_frames[i].h = frames[i].height;
@@ -337,7 +340,7 @@ int zr_plan_describe(const uint8_t *onnx, size_t len, const uint32_t *out_sel, s
     zr::Plan plan;
     std::vector<uint32_t> sel(out_sel, out_sel + n_sel);
     if (!zr::compile_plan(m, sel, plan, err)) return set_err(ZR_ERR_MODEL, err);
-    static const char *kinds[] = {"gemm", "dw", "direct", "elt", "resize", "gap"};
+    static const char *kinds[] = {"gemm", "dw", "direct", "elt", "resize", "gap", "dwpw"};
     static const char *acts[] = {"none", "relu", "clip", "prelu", "sigmoid"};
     std::string t;
     char line[512];
@@ -347,10 +350,10 @@ int zr_plan_describe(const uint8_t *onnx, size_t len, const uint32_t *out_sel, s
                  r.id, r.C, r.H, r.W);
         return std::string(b);
     };
-    snprintf(line, sizeof line, "input %s %dx%dx%d arena_per_image=%lld weights=%zu bytes/img=%.0f flops/img=%.0f\n",
+    snprintf(line, sizeof line, "input %s %dx%dx%d arena_per_image=%lld weights=%zu bytes/img=%.0f flops/img=%.0f fusable=%d\n",
              plan.input_name.c_str(), plan.in_C, plan.in_H, plan.in_W,
              (long long)plan.arena_per_image, plan.weights.size(), plan.bytes_per_image,
-             plan.flops_per_image);
+             plan.flops_per_image, plan.input_fusable ? 1 : 0);
     t += line;
     for (auto &o : plan.outputs) {
         snprintf(line, sizeof line, "output %s per_image=%lld\n", o.name.c_str(), (long long)o.per_image);
@@ -358,8 +361,8 @@ int zr_plan_describe(const uint8_t *onnx, size_t len, const uint32_t *out_sel, s
     }
     for (auto &st : plan.steps) {
         snprintf(line, sizeof line,
-                 "%s in=%s out=%s k=%dx%d s=%d M=%d K=%d KK=%d pre=%s post=%s res=%d rC=%d elt=%d off=%lld oN=%lld oC=%lld oP=%lld\n",
-                 kinds[st.kind], ref(st.in).c_str(), ref(st.out).c_str(), st.kh, st.kw, st.stride,
+                 "%s%s in=%s out=%s k=%dx%d s=%d M=%d K=%d KK=%d pre=%s post=%s res=%d rC=%d elt=%d off=%lld oN=%lld oC=%lld oP=%lld\n",
+                 kinds[st.kind], st.stem ? " stem" : "", ref(st.in).c_str(), ref(st.out).c_str(), st.kh, st.kw, st.stride,
                  st.M, st.K, st.KK, acts[st.pre.kind], acts[st.post.kind], st.res_mode, st.r_C,
                  st.elt_op, (long long)st.out.off, (long long)st.out.o_sN, (long long)st.out.o_sC,
                  (long long)st.out.o_sP);
@@ -474,7 +477,6 @@ static int views_common(zr_session *s, Ctx *c, const zr_frame *frames, size_t nf
     const int64_t hw = (int64_t)s->plan.in_H * s->plan.in_W;
     if (s->plan.in_C != 3) return set_err(ZR_ERR_SHAPE, "view sampling needs a 3-channel input");
     if (!(hi > lo)) return set_err(ZR_ERR_INVALID_ARGUMENT, "ColorMapper range must satisfy end > start");
-    if (int rc = grow(c->input, c->input_floats, (size_t)hw * 3 * nv)) return rc;
     HIP_TRY(hipStreamWaitEvent(stream, c->done, 0));
     if (int rc = upload_views(c, frames, nf, views, view_frame, nv, stream)) return rc;
     zr::PreprocParams p{};
@@ -485,6 +487,9 @@ static int views_common(zr_session *s, Ctx *c, const zr_frame *frames, size_t nf
     p.OH = s->plan.in_H;
     p.lo = lo;
     p.adjust = (hi - lo) / 255.0f;  // nn/mod.rs:162
+    if (s->plan.input_fusable)  // the stem samples the frames itself: no input tensor at all
+        return enqueue(s, c, (int)nv, nullptr, 0, 0, outs, stream, &p);
+    if (int rc = grow(c->input, c->input_floats, (size_t)hw * 3 * nv)) return rc;
     p.out = c->input;
     p.o_sN = hw;                    // CNHW straight into the plan's input layout
     p.o_sC = hw * (int64_t)nv;
@@ -554,6 +559,9 @@ int zr_preprocess_views_async(const zr_frame *frames, size_t n_frames, const zr_
         vd[i] = make_view(views[i], f);
     }
     std::vector<zr::FrameDesc> fd(n_frames);
+    for (size_t i = 0; i < n_frames; i++)
+        if (!frames[i].rgba || frames[i].width == 0 || frames[i].height == 0)
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "empty frame");
     for (size_t i = 0; i < n_frames; i++)
         fd[i] = zr::FrameDesc{frames[i].rgba, frames[i].width, frames[i].height, frames[i].row_stride};
     zr::ViewDesc *dv = nullptr;
@@ -655,6 +663,13 @@ int zr_event_record(void *event, void *stream) {
 int zr_event_synchronize(void *event) {
     HIP_TRY(hipEventSynchronize((hipEvent_t)event));
     return ZR_OK;
+}
+
+int zr_event_query(void *event) {
+    const hipError_t e = hipEventQuery((hipEvent_t)event);
+    if (e == hipSuccess) return ZR_OK;
+    if (e == hipErrorNotReady) return 1;
+    return set_err(ZR_ERR_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
 }
 
 int zr_stream_create(void **stream) {

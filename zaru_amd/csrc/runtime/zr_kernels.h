@@ -143,6 +143,38 @@ struct CandParams {
     float *rec;              // [N][cap][2 + D]
 };
 
+// ---------------------------------------------------------------- fused kernels (fused.hip)
+// Dense KxK stride-S stem conv with Cin = 3 (every model's first layer).  With `pre` the
+// kernel samples its input from RGBA frames through per-image views (K1 fused in front);
+// otherwise it reads the f32 tensor `in`.
+struct StemParams {
+    Plane in;
+    PreprocParams pre;   // frames / views / lo / adjust (used with pre)
+    float *out;
+    int64_t o_sN, o_sC;
+    int IH, IW, OH, OW, N, Cout;
+    int k, stride, pad_t, pad_l;
+    const float *w;      // [>= 32][3][k][k] (zero-padded output channels)
+    const float *bias;   // [>= 32]
+    Act act;
+};
+
+// Depthwise KxK conv feeding a 1x1 conv (BlazeBlock / inverted-residual tail) in one launch.
+// `g` describes the 1x1 conv exactly as for launch_gemm (its x is unused: the depthwise output
+// of each column tile is computed into LDS), `in` is the depthwise input.
+struct DwPwParams {
+    GemmParams g;
+    Plane in;
+    int OW;              // depthwise output width (= positions per row of g's columns)
+    int k, stride, pad_t, pad_l;
+    const float *dw_w;   // [Cin][k*k]
+    const float *dw_b;   // [Cin]
+    Act dw_act;
+};
+
+bool stem_supported(int cin, int k, int stride, int cout);
+bool dwpw_supported(int k, int stride);
+
 // launchers (kernels/*.hip); each returns the symbol of the kernel it launched
 const char *launch_gemm(const GemmParams &p, hipStream_t s);
 const char *launch_dw(const DwParams &p, hipStream_t s);
@@ -152,5 +184,7 @@ const char *launch_resize(const ResizeParams &p, hipStream_t s);
 const char *launch_gap(const GapParams &p, hipStream_t s);
 const char *launch_preproc(const PreprocParams &p, hipStream_t s);
 const char *launch_candidates(const CandParams &p, hipStream_t s);
+const char *launch_stem(const StemParams &p, bool pre, hipStream_t s);
+const char *launch_dwpw(const DwPwParams &p, hipStream_t s);
 
 }  // namespace zr
