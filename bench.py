@@ -172,24 +172,19 @@ def main():
     pipe = H.DetectTrackPipeline(args.workload, device, args.threads,
                                  1 if args.workload == "face" else 4, args.sub_batches,
                                  args.streams == "multi")
-    rec_w = 1 + 8 * 20
-    gather_in = torch.zeros((B, rec_w), dtype=torch.float32, device=f"cuda:{device}")
-    gather_out = torch.zeros((world * B, rec_w), dtype=torch.float32, device=f"cuda:{device}")
+    from zaru_amd import shard
+    gather_in = torch.zeros((B, shard.record_width()), dtype=torch.float32, device=f"cuda:{device}")
 
     pipe.set_frames(flist, forced)
 
     def step():
         pipe.run_frames()
         if world > 1:
-            # one RCCL all-gather of fixed-size detection records per step
-            recs = np.zeros((B, rec_w), np.float32)
-            for f, dets in enumerate(pipe.detections()):
-                recs[f, 0] = len(dets)
-                for k, d in enumerate(dets[:8]):
-                    r = d.bounding_rect().tuple()
-                    recs[f, 1 + 20 * k:1 + 20 * k + 6] = (d.confidence(), d.angle(), *r)
+            # one RCCL all-gather of fixed-size detection records per step;
+            # this rank's frames are global frames rank, rank + world, ... (shard.frames_of_rank)
+            recs = pipe.detection_records(shard.REC_DETS, rank, world)
             gather_in.copy_(torch.from_numpy(recs))
-            dist.all_gather_into_tensor(gather_out, gather_in)
+            shard.all_gather_records(gather_in)
         return pipe.num_rois()
 
     for _ in range(args.warmup):

@@ -14,4 +14,34 @@ __device__ __forceinline__ float apply_act(const Act &a, float v, int c) {
     }
 }
 
+// The same over N values, element r on channel ch(r).  The kind is uniform, so the switch
+// sits outside the loop and every branch is straight-line code the scheduler can interleave
+// (a switch per element would fence every load behind it).
+template <int N, typename ChanFn>
+__device__ __forceinline__ void apply_act_n(const Act &a, float *v, ChanFn ch) {
+    switch (a.kind) {
+    case ACT_RELU:
+#pragma unroll
+        for (int r = 0; r < N; ++r) v[r] = fmaxf(v[r], 0.f);
+        break;
+    case ACT_CLIP:
+#pragma unroll
+        for (int r = 0; r < N; ++r) v[r] = fminf(fmaxf(v[r], a.lo), a.hi);
+        break;
+    case ACT_PRELU: {
+        float s[N];
+#pragma unroll
+        for (int r = 0; r < N; ++r) s[r] = a.slope[ch(r)];
+#pragma unroll
+        for (int r = 0; r < N; ++r) v[r] = v[r] < 0.f ? v[r] * s[r] : v[r];
+        break;
+    }
+    case ACT_SIGMOID:
+#pragma unroll
+        for (int r = 0; r < N; ++r) v[r] = 1.f / (1.f + expf(-v[r]));
+        break;
+    default: break;
+    }
+}
+
 }  // namespace zr

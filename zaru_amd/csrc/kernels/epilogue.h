@@ -4,6 +4,10 @@
 // channels >= r_C of it are zero (the ONNX channel Pad).  The store goes through the output's
 // (sN, sC, sP) strides, which is how graph outputs land in the reference's row-major layout.
 // Also the C/D fragment row map of v_mfma_f32_32x32x2_f32.
+//
+// Addressing: every tensor a launch touches is < 2^31 floats (checked by the runtime), so
+// offsets are 32-bit and added to uniform base pointers (saddr + voffset addressing, no 64-bit
+// VALU address math per element).
 #pragma once
 #include "../runtime/zr_kernels.h"
 #include "act.h"
@@ -16,38 +20,48 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ int mfma32_row(int r, int kh) { return (r & 3) + 8 * (r >> 2) + 4 * kh; }
 
 // One 32x32 accumulator tile of one lane: rows mbase + mfma32_row(r, kh), column (n, q).
-// All residual loads of the tile are issued before any is used (clamped addresses, no branch
-// around a load), so the tile pays one memory latency, not sixteen.
+// Loads (bias, residual, slopes) are all issued before any is used, from clamped addresses:
+// the tile pays one memory latency, not sixteen.
 __device__ __forceinline__ void epilogue_tile(const GemmParams &P, const f32x16 &acc, int n, int q,
                                               int mbase, int kh) {
+    auto chan = [&](int r) {
+        const int m = mbase + mfma32_row(r, kh);
+        return m < P.Mpad ? m : 0;
+    };
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = acc[r] + P.bias[chan(r)];
     float rv[16];
     if (P.res_mode == 1) {
-        const float *rb = P.r + (int64_t)n * P.r_sN + q;
+        const uint32_t rb = (uint32_t)n * (uint32_t)P.r_sN + (uint32_t)q;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int m = mbase + mfma32_row(r, kh);
-            const float v = rb[(int64_t)(m < P.r_C ? m : 0) * P.r_sC];
-            rv[r] = m < P.r_C ? v : 0.f;
+            const float x = P.r[rb + (uint32_t)(m < P.r_C ? m : 0) * (uint32_t)P.r_sC];
+            rv[r] = m < P.r_C ? x : 0.f;
         }
     } else if (P.res_mode == 2) {
         const int y = q / P.out_W, x = q - y * P.out_W;
-        const float *rb = P.r + (int64_t)n * P.r_sN + (int64_t)(2 * y) * P.r_W + 2 * x;
+        const uint32_t rb = (uint32_t)n * (uint32_t)P.r_sN + (uint32_t)((2 * y) * P.r_W + 2 * x);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int m = mbase + mfma32_row(r, kh);
-            const float *s0 = rb + (int64_t)(m < P.r_C ? m : 0) * P.r_sC;
-            const float v = fmaxf(fmaxf(s0[0], s0[1]), fmaxf(s0[P.r_W], s0[P.r_W + 1]));
-            rv[r] = m < P.r_C ? v : 0.f;
+            const uint32_t o = rb + (uint32_t)(m < P.r_C ? m : 0) * (uint32_t)P.r_sC;
+            const float p = fmaxf(fmaxf(P.r[o], P.r[o + 1]), fmaxf(P.r[o + P.r_W], P.r[o + P.r_W + 1]));
+            rv[r] = m < P.r_C ? p : 0.f;
         }
     }
-    float *ob = P.out + (int64_t)n * P.o_sN + (int64_t)q * P.o_sP;
+    apply_act_n<16>(P.pre, v, chan);
+    if (P.res_mode != 0) {  // ONNX Add of the (zero-padded) shortcut
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] += rv[r];
+    }
+    apply_act_n<16>(P.post, v, chan);
+    const uint32_t ob = (uint32_t)n * (uint32_t)P.o_sN + (uint32_t)q * (uint32_t)P.o_sP;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int m = mbase + mfma32_row(r, kh);
-        if (m >= P.M) continue;
-        float v = apply_act(P.pre, acc[r] + P.bias[m], m);
-        if (P.res_mode != 0) v += rv[r];  // ONNX Add of the (zero-padded) shortcut
-        ob[(int64_t)m * P.o_sC] = apply_act(P.post, v, m);
+        if (m < P.M) P.out[ob + (uint32_t)m * (uint32_t)P.o_sC] = v[r];
     }
 }
 

@@ -7,6 +7,7 @@
 //     tail) in one launch; the depthwise output of a column tile lives only in LDS.
 // Reference: the Conv nodes of the four ONNX graphs that ORT/tract execute at
 // crates/zaru/src/nn/mod.rs:483-533, and the image->tensor map at nn/mod.rs:54-73.
+#include <algorithm>
 #include <cstdio>
 
 #include "../runtime/zr_kernels.h"
@@ -159,7 +160,9 @@ __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) 
     const int oy = q / P.OW, ox = q - oy * P.OW;
     const int iy0 = oy * S - P.pad_t, ix0 = ox * S - P.pad_l;
     const int H = P.in.H, W = P.in.W;
-    int off[KK];
+    // tap byte offsets from a channel plane's base, image included (32-bit: see epilogue.h)
+    const uint32_t nbase = (uint32_t)n * (uint32_t)P.in.sN;
+    uint32_t off[KK];
     uint32_t mask = 0;
 #pragma unroll
     for (int ky = 0; ky < K; ++ky)
@@ -167,10 +170,9 @@ __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) 
         for (int kx = 0; kx < K; ++kx) {
             const int iy = iy0 + ky, ix = ix0 + kx;
             const bool ok = iy >= 0 && iy < H && ix >= 0 && ix < W;
-            off[ky * K + kx] = ok ? iy * W + ix : 0;
+            off[ky * K + kx] = (nbase + (ok ? (uint32_t)(iy * W + ix) : 0u)) * 4u;  // bytes
             mask |= (ok ? 1u : 0u) << (ky * K + kx);
         }
-    const float *src = P.in.p + (int64_t)n * P.in.sN;
 
     f32x16 acc[MTW][NTW];
 #pragma unroll
@@ -185,10 +187,11 @@ __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) 
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int c = kc + dc + CPAR * i;
-            const float *pl = src + (int64_t)(c < Cin ? c : Cin - 1) * P.in.sC;
+            const char *pl = (const char *)(P.in.p + (size_t)(uint32_t)(c < Cin ? c : Cin - 1) * (uint32_t)P.in.sC);
 #pragma unroll
-            for (int t = 0; t < KK; ++t) tap[i][t] = pl[off[t]];
+            for (int t = 0; t < KK; ++t) tap[i][t] = *(const float *)(pl + off[t]);
         }
+        float dv[PER];
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int c = kc + dc + CPAR * i;
@@ -197,9 +200,14 @@ __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) 
             float a = P.dw_b[cl];
 #pragma unroll
             for (int t = 0; t < KK; ++t) a = __builtin_fmaf(w[t], ((mask >> t) & 1u) ? tap[i][t] : 0.f, a);
-            a = apply_act(P.dw_act, a, cl);
-            sD[dc + CPAR * i][dj] = c < Cin ? a : 0.f;
+            dv[i] = a;
         }
+        apply_act_n<PER>(P.dw_act, dv, [&](int i) {
+            const int c = kc + dc + CPAR * i;
+            return c < Cin ? c : Cin - 1;
+        });
+#pragma unroll
+        for (int i = 0; i < PER; ++i) sD[dc + CPAR * i][dj] = kc + dc + CPAR * i < Cin ? dv[i] : 0.f;
         for (int i = tid; i < FKC * BM; i += 256) {
             const int r = i / BM, cc = i - r * BM;
             const int k = kc + r, m = m0 + cc;
@@ -230,6 +238,113 @@ __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) 
 #pragma unroll
         for (int t = 0; t < MTW; ++t) epilogue_tile(G, acc[t][u], on, oq, m0 + (wm * MTW + t) * 32, kh);
     }
+}
+
+// Row-staged variant for the high-resolution, few-channel layers (planes of >= 128 positions,
+// <= 96 output channels), where the tap-per-lane form above is VALU-bound on address math and
+// padding masks.  A tile is 128 consecutive positions of ONE image; per chunk of RFKC channels
+// the input rows those positions need (full padded width, zeros where the ONNX padding is) are
+// staged in LDS with coalesced row loads, and each depthwise tap is then one ds_read plus one FMA.
+constexpr int RBN = 128, RFKC = 8;
+
+template <int K, int S, int MT>
+__global__ __launch_bounds__(256) void dwpw_rows_kernel(const DwPwParams P, int tpi, int ntiles, int rmax) {
+    constexpr int PER = RFKC / 2;  // depthwise outputs per thread per chunk (2 channels in parallel)
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const GemmParams &G = P.g;
+    const int Wp = (P.OW - 1) * S + K;          // staged row width (covers every tap)
+    float *sIn = smem;                          // [RFKC][rmax][Wp]
+    float *sD = sIn + RFKC * rmax * Wp;         // [RFKC][RBN]
+    float *sW = sD + RFKC * RBN;                // [RFKC][MT*32]
+
+    const int cpx = gridDim.x >> 3;  // gridDim.x is a multiple of 8
+    const int tile = (blockIdx.x & 7) * cpx + (blockIdx.x >> 3);
+    if (tile >= ntiles) return;  // whole workgroup, before any barrier
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kh = lane >> 5, col = lane & 31;
+    const int n = tile / tpi, q0 = (tile - n * tpi) * RBN;
+    const int Pq = G.P, H = P.in.H, W = P.in.W, Cin = G.K;
+    const int oy_a = q0 / P.OW, oy_b = min(q0 + RBN - 1, Pq - 1) / P.OW;
+    const int iy_a = oy_a * S - P.pad_t;
+    const int R = (oy_b - oy_a) * S + K;  // <= rmax
+
+    // depthwise role: position dq of the tile, channels dc, dc + 2, ... of each chunk
+    const int dq = tid & (RBN - 1);
+    const int dc = __builtin_amdgcn_readfirstlane(tid >> 7);
+    const int qd = min(q0 + dq, Pq - 1);
+    const int oy = qd / P.OW, ox = qd - oy * P.OW;
+    const int lb = (oy * S - P.pad_t - iy_a) * Wp + ox * S;  // staged index of tap (0, 0)
+    const uint32_t nbase = (uint32_t)n * (uint32_t)P.in.sN;
+
+    f32x16 acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+    for (int kc = 0; kc < Cin; kc += RFKC) {
+        // 1. stage rows iy_a .. iy_a + R - 1 of RFKC channels; a wave per row, lanes along x
+        for (int row = wave; row < RFKC * R; row += 4) {
+            const int c = row / R, r = row - c * R;
+            const int ch = kc + c < Cin ? kc + c : Cin - 1;
+            const int iy = iy_a + r;
+            const bool rok = iy >= 0 && iy < H && kc + c < Cin;
+            const float *src = P.in.p + (size_t)(uint32_t)ch * (uint32_t)P.in.sC;
+            const uint32_t rowoff = nbase + (uint32_t)(rok ? iy : 0) * (uint32_t)W;
+            float *dst = sIn + (c * rmax + r) * Wp;
+#pragma unroll 2
+            for (int x = lane; x < Wp; x += 64) {
+                const int ix = x - P.pad_l;
+                const bool ok = rok && ix >= 0 && ix < W;
+                const float v = src[rowoff + (uint32_t)(ok ? ix : 0)];
+                dst[x] = ok ? v : 0.f;
+            }
+        }
+        // 2. the chunk of the transposed 1x1 weights
+        for (int i = tid; i < RFKC * MT * 32; i += 256) {
+            const int r = i / (MT * 32), cc = i - r * (MT * 32);
+            const int k = kc + r;
+            sW[i] = (k < Cin && cc < G.Mpad) ? G.wt[(int64_t)k * G.Mpad + cc] : 0.f;
+        }
+        __syncthreads();
+        // 3. depthwise from LDS
+        float dv[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int c = dc + 2 * i;
+            const int cl = kc + c < Cin ? kc + c : Cin - 1;
+            const float *w = P.dw_w + cl * (K * K);
+            const float *t0 = sIn + c * rmax * Wp + lb;
+            float a = P.dw_b[cl];
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx) a = __builtin_fmaf(w[ky * K + kx], t0[ky * Wp + kx], a);
+            dv[i] = a;
+        }
+        apply_act_n<PER>(P.dw_act, dv, [&](int i) {
+            const int c = kc + dc + 2 * i;
+            return c < Cin ? c : Cin - 1;
+        });
+#pragma unroll
+        for (int i = 0; i < PER; ++i) sD[(dc + 2 * i) * RBN + dq] = kc + dc + 2 * i < Cin ? dv[i] : 0.f;
+        __syncthreads();
+        // 4. the 1x1 conv over the chunk
+#pragma unroll
+        for (int s = 0; s < RFKC / 2; ++s) {
+            const float b = sD[(2 * s + kh) * RBN + wave * 32 + col];
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(sW[(2 * s + kh) * (MT * 32) + t * 32 + col], b,
+                                                              acc[t], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+
+    const int q = q0 + wave * 32 + col;
+    if (q >= Pq) return;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) epilogue_tile(G, acc[t], n, q, t * 32, kh);
 }
 
 bool dwpw_supported(int k, int stride) { return (k == 3 || k == 5) && (stride == 1 || stride == 2); }
@@ -276,9 +391,47 @@ const char *dwpw_layout(const DwPwParams &p, const DwPwLayout &l, hipStream_t s)
 
 }  // namespace
 
-// Layout choice: no M split unless Mpad > 256, at most 1/3 padded rows; among those, the
-// widest column tile that still gives >= 4 workgroups per CU (else the most workgroups).
+namespace {
+
+template <int K, int S, int MT>
+const char *dwpw_rows_go(const DwPwParams &p, hipStream_t s) {
+    const int P = p.g.P, tpi = (P + RBN - 1) / RBN, ntiles = tpi * p.g.ncols / P;
+    // the most input rows any tile needs
+    int rmax = 0;
+    for (int t = 0; t < tpi; t++) {
+        const int q0 = t * RBN, a = q0 / p.OW, b = std::min(q0 + RBN - 1, P - 1) / p.OW;
+        rmax = std::max(rmax, (b - a) * S + K);
+    }
+    const int Wp = (p.OW - 1) * S + K;
+    const size_t lds = sizeof(float) * ((size_t)RFKC * rmax * Wp + RFKC * RBN + RFKC * MT * 32);
+    dim3 grid((ntiles + 7) / 8 * 8);
+    hipLaunchKernelGGL((dwpw_rows_kernel<K, S, MT>), grid, dim3(256), lds, s, p, tpi, ntiles, rmax);
+    static char names[2][2][4][48];
+    char *nm = names[K == 5][S == 2][MT];
+    if (!nm[0]) snprintf(nm, 48, "dwpw_rows_kernel<%d,%d,%dx%d>", K, S, MT * 32, RBN);
+    return nm;
+}
+
+template <int K, int S>
+const char *dwpw_rows_mt(const DwPwParams &p, hipStream_t s) {
+    switch (p.g.Mpad / 32) {
+    case 1: return dwpw_rows_go<K, S, 1>(p, s);
+    case 2: return dwpw_rows_go<K, S, 2>(p, s);
+    default: return dwpw_rows_go<K, S, 3>(p, s);
+    }
+}
+
+}  // namespace
+
+// Layout choice.  High-resolution planes with few output channels take the row-staged kernel.
+// Otherwise: no M split unless Mpad > 256, at most 1/3 padded rows; among those, the widest
+// column tile that still gives >= 4 workgroups per CU (else the most workgroups).
 const char *launch_dwpw(const DwPwParams &p, hipStream_t s) {
+    const int Wp = (p.OW - 1) * p.stride + p.k;
+    if (p.g.P >= RBN && p.g.Mpad <= 96 && Wp <= 160 && p.g.ncols % p.g.P == 0) {
+        if (p.k == 3) return p.stride == 1 ? dwpw_rows_mt<3, 1>(p, s) : dwpw_rows_mt<3, 2>(p, s);
+        return p.stride == 1 ? dwpw_rows_mt<5, 1>(p, s) : dwpw_rows_mt<5, 2>(p, s);
+    }
     const DwPwLayout *best = nullptr;
     int64_t best_wgs = 0;
     for (const DwPwLayout &l : kLayouts) {
