@@ -9,6 +9,7 @@
 // crates/zaru/src/nn/mod.rs:483-533, and the image->tensor map at nn/mod.rs:54-73.
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 
 #include "../runtime/zr_kernels.h"
 #include "act.h"
@@ -97,7 +98,10 @@ static const char *stem_go(const StemParams &p, bool pre, hipStream_t s) {
     dim3 grid(tiles, p.N);
     if (pre) hipLaunchKernelGGL((stem_kernel<K, S, CO, true>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((stem_kernel<K, S, CO, false>), grid, dim3(256), 0, s, p);
-    return pre ? "stem_kernel<pre>" : "stem_kernel";
+    static char names[2][2][3][2][40];
+    char *nm = names[K == 5][S == 2][CO / 8 - 2][pre];
+    if (!nm[0]) snprintf(nm, 40, "stem_kernel<%d,%d,%d,%s>", K, S, CO, pre ? "true" : "false");
+    return nm;
 }
 
 template <int K, int S>
@@ -283,21 +287,37 @@ __global__ __launch_bounds__(256) void dwpw_rows_kernel(const DwPwParams P, int 
         for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
     for (int kc = 0; kc < Cin; kc += RFKC) {
-        // 1. stage rows iy_a .. iy_a + R - 1 of RFKC channels; a wave per row, lanes along x
-        for (int row = wave; row < RFKC * R; row += 4) {
-            const int c = row / R, r = row - c * R;
-            const int ch = kc + c < Cin ? kc + c : Cin - 1;
-            const int iy = iy_a + r;
-            const bool rok = iy >= 0 && iy < H && kc + c < Cin;
-            const float *src = P.in.p + (size_t)(uint32_t)ch * (uint32_t)P.in.sC;
-            const uint32_t rowoff = nbase + (uint32_t)(rok ? iy : 0) * (uint32_t)W;
-            float *dst = sIn + (c * rmax + r) * Wp;
-#pragma unroll 2
-            for (int x = lane; x < Wp; x += 64) {
-                const int ix = x - P.pad_l;
-                const bool ok = rok && ix >= 0 && ix < W;
-                const float v = src[rowoff + (uint32_t)(ok ? ix : 0)];
-                dst[x] = ok ? v : 0.f;
+        // 1. stage rows iy_a .. iy_a + R - 1 of RFKC channels: a wave per row, lanes along x
+        //    (Wp <= 128: two loads per lane per row), 4 rows per wave in flight at once
+        const int nrows = RFKC * R;
+        for (int row0 = wave; row0 < nrows; row0 += 16) {
+            float v[4][2];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int row = min(row0 + 4 * k, nrows - 1);
+                const int c = row / R, r = row - c * R;
+                const int ch = kc + c < Cin ? kc + c : Cin - 1;
+                const int iy = iy_a + r;
+                const bool rok = iy >= 0 && iy < H && kc + c < Cin;
+                const float *src = P.in.p + (size_t)(uint32_t)ch * (uint32_t)P.in.sC;
+                const uint32_t rowoff = nbase + (uint32_t)(rok ? iy : 0) * (uint32_t)W;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int ix = lane + 64 * h - P.pad_l;
+                    const bool ok = rok && ix >= 0 && ix < W;
+                    const float x = src[rowoff + (uint32_t)(ok ? ix : 0)];
+                    v[k][h] = ok ? x : 0.f;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int row = row0 + 4 * k;
+                if (row >= nrows) break;
+                const int c = row / R, r = row - c * R;
+                float *dst = sIn + (c * rmax + r) * Wp;
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    if (lane + 64 * h < Wp) dst[lane + 64 * h] = v[k][h];
             }
         }
         // 2. the chunk of the transposed 1x1 weights
@@ -368,9 +388,9 @@ const char *dwpw_go(const DwPwParams &p, hipStream_t s) {
     const int mb = (p.g.Mpad + BM - 1) / BM;
     dim3 grid((nct + 7) / 8 * 8, mb);
     hipLaunchKernelGGL((dwpw_kernel<K, S, WM, MTW, 1>), grid, dim3(256), 0, s, p, nct);
-    static char names[2][2][5][5][40];
+    static char names[2][2][5][5][40];  // the symbol as rocprofv3 prints it, spaces removed
     char *nm = names[K == 5][S == 2][WM][MTW];
-    if (!nm[0]) snprintf(nm, 40, "dwpw_kernel<%d,%d,%dx%d>", K, S, BM, BN);
+    if (!nm[0]) snprintf(nm, 40, "dwpw_kernel<%d,%d,%d,%d,1>", K, S, WM, MTW);
     return nm;
 }
 
@@ -408,7 +428,7 @@ const char *dwpw_rows_go(const DwPwParams &p, hipStream_t s) {
     hipLaunchKernelGGL((dwpw_rows_kernel<K, S, MT>), grid, dim3(256), lds, s, p, tpi, ntiles, rmax);
     static char names[2][2][4][48];
     char *nm = names[K == 5][S == 2][MT];
-    if (!nm[0]) snprintf(nm, 48, "dwpw_rows_kernel<%d,%d,%dx%d>", K, S, MT * 32, RBN);
+    if (!nm[0]) snprintf(nm, 48, "dwpw_rows_kernel<%d,%d,%d>", K, S, MT);
     return nm;
 }
 
@@ -427,8 +447,12 @@ const char *dwpw_rows_mt(const DwPwParams &p, hipStream_t s) {
 // Otherwise: no M split unless Mpad > 256, at most 1/3 padded rows; among those, the widest
 // column tile that still gives >= 4 workgroups per CU (else the most workgroups).
 const char *launch_dwpw(const DwPwParams &p, hipStream_t s) {
+    static const bool rows_on = [] {  // A/B switch while the staged form is being tuned
+        const char *e = std::getenv("ZR_DWPW_ROWS");
+        return e && e[0] == '1';
+    }();
     const int Wp = (p.OW - 1) * p.stride + p.k;
-    if (p.g.P >= RBN && p.g.Mpad <= 96 && Wp <= 160 && p.g.ncols % p.g.P == 0) {
+    if (rows_on && p.g.P >= RBN && p.g.Mpad <= 96 && Wp <= 128 && p.g.ncols % p.g.P == 0) {
         if (p.k == 3) return p.stride == 1 ? dwpw_rows_mt<3, 1>(p, s) : dwpw_rows_mt<3, 2>(p, s);
         return p.stride == 1 ? dwpw_rows_mt<5, 1>(p, s) : dwpw_rows_mt<5, 2>(p, s);
     }
