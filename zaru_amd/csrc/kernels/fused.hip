@@ -18,6 +18,8 @@
 
 namespace zr {
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 // ------------------------------------------------------------------ stem
 constexpr int STH = 8, STW = 32;  // output tile: 8 rows x 32 columns, one pixel per thread
 
@@ -67,25 +69,33 @@ __global__ __launch_bounds__(256) void stem_kernel(const StemParams P) {
     }
     __syncthreads();
     const int ly = threadIdx.x / STW, lx = threadIdx.x - ly * STW;
-    float acc[CO];
+    f32x2 acc[CO / 2];
 #pragma unroll
-    for (int o = 0; o < CO; ++o) acc[o] = 0.f;
+    for (int o = 0; o < CO / 2; ++o) acc[o] = (f32x2)(0.f);
     for (int c = 0; c < 3; ++c)
 #pragma unroll
         for (int ky = 0; ky < K; ++ky)
 #pragma unroll
             for (int kx = 0; kx < K; ++kx) {
                 const float v = patch[c][ly * S + ky][lx * S + kx];
-                const float *w = P.w + (c * K + ky) * K + kx;  // uniform: scalar loads
+                // weights [3][K][K][32]: uniform, so scalar loads feeding v_pk_fma_f32
+                const f32x2 *w2 = (const f32x2 *)(P.w + ((c * K + ky) * K + kx) * 32);
 #pragma unroll
-                for (int o = 0; o < CO; ++o) acc[o] = __builtin_fmaf(w[o * 3 * K * K], v, acc[o]);
+                for (int o = 0; o < CO / 2; ++o) acc[o] = __builtin_elementwise_fma(w2[o], (f32x2)(v), acc[o]);
             }
     const int oy = ty0 + ly, ox = tx0 + lx;
     if (oy >= P.OH || ox >= P.OW) return;
+    float vo[CO];
+#pragma unroll
+    for (int o = 0; o < CO / 2; ++o) {
+        vo[2 * o] = acc[o].x + P.bias[2 * o];
+        vo[2 * o + 1] = acc[o].y + P.bias[2 * o + 1];
+    }
+    apply_act_n<CO>(P.act, vo, [](int o) { return o; });
     float *dst = P.out + (int64_t)n * P.o_sN + (int64_t)oy * P.OW + ox;
 #pragma unroll
     for (int o = 0; o < CO; ++o)
-        if (o < P.Cout) dst[(int64_t)o * P.o_sC] = apply_act(P.act, acc[o] + P.bias[o], o);
+        if (o < P.Cout) dst[(int64_t)o * P.o_sC] = vo[o];
 }
 
 bool stem_supported(int cin, int k, int stride, int cout) {
@@ -367,6 +377,134 @@ __global__ __launch_bounds__(256) void dwpw_rows_kernel(const DwPwParams P, int 
     for (int t = 0; t < MT; ++t) epilogue_tile(G, acc[t], n, q, t * 32, kh);
 }
 
+// VALU form for the high-resolution layers with few channels (Cin * Cout <= 1600: the
+// BlazeBlocks at 96^2/64^2/48^2/32^2), where the MFMA tile would be mostly padding and the
+// per-lane tap loads cost more memory instructions than the bytes they bring.  One thread per
+// output position, 256 positions of one image per workgroup:
+//   1. per chunk of VFKC input channels, the input rows the tile needs are staged in LDS with
+//      16-byte row loads (zero columns/rows where the ONNX padding is);
+//   2. each thread computes its depthwise value per channel from LDS (one ds_read + FMA per
+//      tap) and accumulates the 1x1 conv into CO registers with v_pk_fma_f32, the weights
+//      coming through the scalar cache (they are uniform across the workgroup);
+//   3. epilogue per output channel: bias, activation, residual (+pad/+pool), activation, one
+//      coalesced store per channel.
+constexpr int VTQ = 256, VFKC = 8;
+
+// a / b for 0 <= a < 2^22 through the f32 reciprocal, corrected to the exact quotient
+__device__ __forceinline__ int qdiv(int a, int b, float inv_b) {
+    int q = (int)((float)a * inv_b);
+    const int r = a - q * b;
+    q += r >= b ? 1 : 0;
+    q -= r < 0 ? 1 : 0;
+    return q;
+}
+
+template <int K, int S, int CO>
+__global__ __launch_bounds__(256) void dwpw_valu_kernel(const DwPwParams P, int tpi, int ntiles, int rmax, int lw) {
+    extern __shared__ __attribute__((aligned(16))) float sIn[];  // [VFKC * rows][lw]
+    const GemmParams &G = P.g;
+    const int cpx = gridDim.x >> 3;  // gridDim.x is a multiple of 8
+    const int tile = (blockIdx.x & 7) * cpx + (blockIdx.x >> 3);
+    if (tile >= ntiles) return;  // whole workgroup, before any barrier
+    const int tid = threadIdx.x;
+    const int n = tile / tpi, q0 = (tile - n * tpi) * VTQ;
+    const int Pq = G.P, H = P.in.H, W = P.in.W, Cin = G.K, OW = P.OW;
+    const int oy_a = q0 / OW, oy_b = min(q0 + VTQ - 1, Pq - 1) / OW;
+    const int iy_a = oy_a * S - P.pad_t;
+    const int R = (oy_b - oy_a) * S + K;  // <= rmax
+    const int q = min(q0 + tid, Pq - 1);
+    const int oy = q / OW, ox = q - oy * OW;
+    // LDS row layout: 4 zero floats, the W input values, >= 4 zero floats (lw % 4 == 0)
+    const int lb = (oy * S - P.pad_t - iy_a) * lw + 4 - P.pad_l + ox * S;  // tap (0, 0)
+    const uint32_t nbase = (uint32_t)n * (uint32_t)P.in.sN;
+    const int srow = (W >> 2) + 2;  // float4 slots per staged row
+    const float inv_srow = 1.f / (float)srow, inv_R = 1.f / (float)R;
+
+    f32x2 acc[CO / 2];
+#pragma unroll
+    for (int i = 0; i < CO / 2; ++i) acc[i] = (f32x2)(0.f);
+
+    for (int kc = 0; kc < Cin; kc += VFKC) {
+        const int total = VFKC * R * srow;
+        for (int base = 0; base < total; base += 1024) {
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int sl = min(base + tid + 256 * u, total - 1);
+                const int cr = qdiv(sl, srow, inv_srow), sx = sl - cr * srow;
+                const int c = qdiv(cr, R, inv_R), r = cr - c * R;
+                const int iy = iy_a + r, ch = kc + c, xv = sx - 1;
+                const bool ok = iy >= 0 && iy < H && ch < Cin && xv >= 0 && 4 * xv < W;
+                const float *src = P.in.p + (size_t)(uint32_t)(ch < Cin ? ch : Cin - 1) * (uint32_t)P.in.sC;
+                const float4 x = *(const float4 *)(src + nbase + (uint32_t)(ok ? iy * W + 4 * xv : 0));
+                v[u] = ok ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int sl = base + tid + 256 * u;
+                if (sl < total) {
+                    const int cr = qdiv(sl, srow, inv_srow), sx = sl - cr * srow;
+                    *(float4 *)(sIn + cr * lw + 4 * sx) = v[u];
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < VFKC; ++c) {
+            const int ch = kc + c;
+            if (ch >= Cin) break;
+            const float *t0 = sIn + c * R * lw + lb;
+            const float *w = P.dw_w + ch * (K * K);
+            float d = P.dw_b[ch];
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx) d = __builtin_fmaf(w[ky * K + kx], t0[ky * lw + kx], d);
+            d = apply_act(P.dw_act, d, ch);
+            const f32x2 *w2 = (const f32x2 *)(G.wt + (size_t)ch * G.Mpad);  // [Kpad][Mpad]
+#pragma unroll
+            for (int i = 0; i < CO / 2; ++i) acc[i] = __builtin_elementwise_fma(w2[i], (f32x2)(d), acc[i]);
+        }
+        __syncthreads();
+    }
+
+    if (q0 + tid >= Pq) return;
+    float v[CO];
+#pragma unroll
+    for (int i = 0; i < CO / 2; ++i) {
+        v[2 * i] = acc[i].x + G.bias[2 * i];
+        v[2 * i + 1] = acc[i].y + G.bias[2 * i + 1];
+    }
+    float rv[CO];
+    if (G.res_mode == 1) {
+        const uint32_t rb = (uint32_t)n * (uint32_t)G.r_sN + (uint32_t)q;
+#pragma unroll
+        for (int m = 0; m < CO; ++m) {
+            const float x = G.r[rb + (uint32_t)(m < G.r_C ? m : 0) * (uint32_t)G.r_sC];
+            rv[m] = m < G.r_C ? x : 0.f;
+        }
+    } else if (G.res_mode == 2) {
+        const uint32_t rb = (uint32_t)n * (uint32_t)G.r_sN + (uint32_t)((2 * oy) * G.r_W + 2 * ox);
+#pragma unroll
+        for (int m = 0; m < CO; ++m) {
+            const uint32_t o = rb + (uint32_t)(m < G.r_C ? m : 0) * (uint32_t)G.r_sC;
+            const float p = fmaxf(fmaxf(G.r[o], G.r[o + 1]), fmaxf(G.r[o + G.r_W], G.r[o + G.r_W + 1]));
+            rv[m] = m < G.r_C ? p : 0.f;
+        }
+    }
+    auto chan = [](int m) { return m; };
+    apply_act_n<CO>(G.pre, v, chan);
+    if (G.res_mode != 0) {
+#pragma unroll
+        for (int m = 0; m < CO; ++m) v[m] += rv[m];
+    }
+    apply_act_n<CO>(G.post, v, chan);
+    const uint32_t ob = (uint32_t)n * (uint32_t)G.o_sN + (uint32_t)q * (uint32_t)G.o_sP;
+#pragma unroll
+    for (int m = 0; m < CO; ++m)
+        if (m < G.M) G.out[ob + (uint32_t)m * (uint32_t)G.o_sC] = v[m];
+}
+
 bool dwpw_supported(int k, int stride) { return (k == 3 || k == 5) && (stride == 1 || stride == 2); }
 
 namespace {
@@ -441,9 +579,49 @@ const char *dwpw_rows_mt(const DwPwParams &p, hipStream_t s) {
     }
 }
 
+template <int K, int S, int CO>
+const char *dwpw_valu_go(const DwPwParams &p, hipStream_t s) {
+    const int P = p.g.P, tpi = (P + VTQ - 1) / VTQ, ntiles = tpi * (p.g.ncols / P);
+    int rmax = 0;
+    for (int t = 0; t < tpi; t++) {
+        const int q0 = t * VTQ, a = q0 / p.OW, b = std::min(q0 + VTQ - 1, P - 1) / p.OW;
+        rmax = std::max(rmax, (b - a) * S + K);
+    }
+    const int lw = p.in.W + 8;
+    const size_t lds = sizeof(float) * (size_t)VFKC * rmax * lw;
+    dim3 grid((ntiles + 7) / 8 * 8);
+    hipLaunchKernelGGL((dwpw_valu_kernel<K, S, CO>), grid, dim3(256), lds, s, p, tpi, ntiles, rmax, lw);
+    static char names[2][2][5][48];
+    char *nm = names[K == 5][S == 2][CO / 16];
+    if (!nm[0]) snprintf(nm, 48, "dwpw_valu_kernel<%d,%d,%d>", K, S, CO);
+    return nm;
+}
+
+template <int K, int S>
+const char *dwpw_valu_co(const DwPwParams &p, hipStream_t s) {
+    if (p.g.M <= 16) return dwpw_valu_go<K, S, 16>(p, s);
+    if (p.g.M <= 32) return dwpw_valu_go<K, S, 32>(p, s);
+    if (p.g.M <= 48) return dwpw_valu_go<K, S, 48>(p, s);
+    return dwpw_valu_go<K, S, 64>(p, s);
+}
+
 }  // namespace
 
-// Layout choice.  High-resolution planes with few output channels take the row-staged kernel.
+// The VALU form applies to (see dwpw_valu_kernel): >= 256 positions per image, W % 4 == 0
+// (16-byte row loads), Cout <= 64, Cin * Cout <= 1600, staged rows within 64 KiB.
+static bool valu_form(const DwPwParams &p) {
+    static const int mode = [] {  // ZR_DWPW_VALU=0 disables the form (A/B runs)
+        const char *e = std::getenv("ZR_DWPW_VALU");
+        return e ? std::atoi(e) : 1;
+    }();
+    if (!mode || p.g.P < VTQ || p.in.W % 4 != 0 || p.g.M > 64 || p.g.K * p.g.M > 1600) return false;
+    if (p.g.ncols % p.g.P != 0) return false;
+    const int rows = (VTQ / p.OW + 2) * p.stride + p.k;
+    return sizeof(float) * (size_t)VFKC * rows * (p.in.W + 8) <= 64 * 1024;
+}
+
+// Layout choice.  High-resolution planes with few channels take the VALU form; otherwise
+// (MFMA form) high-resolution planes with few output channels may take the row-staged kernel.
 // Otherwise: no M split unless Mpad > 256, at most 1/3 padded rows; among those, the widest
 // column tile that still gives >= 4 workgroups per CU (else the most workgroups).
 const char *launch_dwpw(const DwPwParams &p, hipStream_t s) {
@@ -451,6 +629,10 @@ const char *launch_dwpw(const DwPwParams &p, hipStream_t s) {
         const char *e = std::getenv("ZR_DWPW_ROWS");
         return e && e[0] == '1';
     }();
+    if (valu_form(p)) {
+        if (p.k == 3) return p.stride == 1 ? dwpw_valu_co<3, 1>(p, s) : dwpw_valu_co<3, 2>(p, s);
+        return p.stride == 1 ? dwpw_valu_co<5, 1>(p, s) : dwpw_valu_co<5, 2>(p, s);
+    }
     const int Wp = (p.OW - 1) * p.stride + p.k;
     if (rows_on && p.g.P >= RBN && p.g.Mpad <= 96 && Wp <= 128 && p.g.ncols % p.g.P == 0) {
         if (p.k == 3) return p.stride == 1 ? dwpw_rows_mt<3, 1>(p, s) : dwpw_rows_mt<3, 2>(p, s);

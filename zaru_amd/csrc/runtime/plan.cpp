@@ -387,8 +387,10 @@ bool Compiler::lower_conv(const OnnxNode &nd) {
         s.M = Mo;
         s.stem = kh == kw && stem_supported(Cin, kh, (int)st[0], Mo);
         std::vector<float> wf = w->f;
-        if (s.stem) {  // stem_kernel reads 32 output channels of weights unconditionally
-            wf.resize((size_t)32 * Cin * kh * kw, 0.f);
+        if (s.stem) {  // stem_kernel: [Cin][kh][kw][32], output channel innermost, zero-padded
+            wf.assign((size_t)32 * Cin * kh * kw, 0.f);
+            for (int m = 0; m < Mo; m++)
+                for (int t = 0; t < Cin * kh * kw; t++) wf[(size_t)t * 32 + m] = w->f[(size_t)m * Cin * kh * kw + t];
             bias.resize(32, 0.f);
         }
         s.w_off = push_weights(wf);

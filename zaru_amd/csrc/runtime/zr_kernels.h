@@ -154,7 +154,7 @@ struct StemParams {
     int64_t o_sN, o_sC;
     int IH, IW, OH, OW, N, Cout;
     int k, stride, pad_t, pad_l;
-    const float *w;      // [>= 32][3][k][k] (zero-padded output channels)
+    const float *w;      // [3][k][k][32] (output channel innermost, zero-padded to 32)
     const float *bias;   // [>= 32]
     Act act;
 };
