@@ -64,6 +64,22 @@ def test_batch_independence(nets, model):
         assert np.array_equal(a[0], b[1]) and np.array_equal(a[0], b[3])
 
 
+@pytest.mark.parametrize("model", list(MODELS))
+def test_large_batch_matches_single_images(nets, model):
+    """Kernel layouts are chosen per launch from the batch size (fused.hip launch_dwpw), so a
+    production-size batch runs different tilings than the small parity batches.  Every
+    tiling keeps each column's arithmetic order, so results must match bit for bit."""
+    s, lo, hi = MODELS[model]
+    rng = np.random.default_rng(13)
+    n = 520
+    x = codes_to_input(rng.integers(0, 256, size=(n, 3, s, s), dtype=np.uint8), lo, hi)
+    many = nets[model].estimate(x)
+    for i in (0, 1, 257, n - 1):
+        one = nets[model].estimate(x[i:i + 1])
+        for a, b in zip(one, many):
+            assert np.array_equal(a[0], b[i]), (model, i)
+
+
 def test_detects_face(nets, golden_dir, kat):
     """face/detection.rs:164-173 through the HIP runner."""
     g = np.load(os.path.join(golden_dir, "sad_linus_face.npz"))

@@ -377,8 +377,8 @@ __global__ __launch_bounds__(256) void dwpw_rows_kernel(const DwPwParams P, int 
     for (int t = 0; t < MT; ++t) epilogue_tile(G, acc[t], n, q, t * 32, kh);
 }
 
-// VALU form for the high-resolution layers with few channels (Cin * Cout <= 1600: the
-// BlazeBlocks at 96^2/64^2/48^2/32^2), where the MFMA tile would be mostly padding and the
+// VALU form for the high-resolution layers with few channels (Cin * Cout <= 2048: the
+// BlazeBlocks at 96^2 .. 32^2), where the MFMA tile would be mostly padding and the
 // per-lane tap loads cost more memory instructions than the bytes they bring.  One thread per
 // output position, 256 positions of one image per workgroup:
 //   1. per chunk of VFKC input channels, the input rows the tile needs are staged in LDS with
@@ -449,7 +449,7 @@ __global__ __launch_bounds__(256) void dwpw_valu_kernel(const DwPwParams P, int 
             }
         }
         __syncthreads();
-#pragma unroll
+#pragma unroll 2
         for (int c = 0; c < VFKC; ++c) {
             const int ch = kc + c;
             if (ch >= Cin) break;
@@ -503,6 +503,129 @@ __global__ __launch_bounds__(256) void dwpw_valu_kernel(const DwPwParams P, int 
 #pragma unroll
     for (int m = 0; m < CO; ++m)
         if (m < G.M) G.out[ob + (uint32_t)m * (uint32_t)G.o_sC] = v[m];
+}
+
+// Image-tile MFMA form for the low-resolution layers (planes of <= 256 positions: 16^2 ... 3^2,
+// with up to 256 channels).  A workgroup owns G whole images (G * P <= 256 columns), so the
+// depthwise input of a channel chunk is the contiguous run of G * P floats of each channel
+// (CNHW): it is copied into zero-bordered LDS planes once, and each tap is then one ds_read.
+// The 1x1 conv runs as v_mfma_f32_32x32x2_f32 with the 4 waves along N (NTW 32-column tiles
+// each) and all MT row tiles per wave; Mpad > MT*32 splits M across workgroups.
+constexpr int IFKC = 16, IBN = 256;
+
+template <int K, int S, int MT, int NTW>
+__global__ __launch_bounds__(256) void dwpw_img_kernel(const DwPwParams P, int G, int ntiles, int nimg) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const GemmParams &G_ = P.g;
+    const int H = P.in.H, W = P.in.W, Pin = H * W, Pq = G_.P, OW = P.OW;
+    const int Hp = (P.OW == 0) ? 0 : ((Pq / OW) - 1) * S + K, Wp = (OW - 1) * S + K;  // padded plane
+    const int plane = Hp * Wp;
+    float *sIn = smem;                         // [IFKC][G][Hp][Wp]
+    float *sD = sIn + IFKC * G * plane;        // [IFKC][IBN]
+    float *sW = sD + IFKC * IBN;               // [IFKC][MT*32]
+
+    const int cpx = gridDim.x >> 3;  // gridDim.x is a multiple of 8
+    const int tile = (blockIdx.x & 7) * cpx + (blockIdx.x >> 3);
+    if (tile >= ntiles) return;  // whole workgroup, before any barrier
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kh = lane >> 5, col = lane & 31;
+    const int n0 = tile * G, g_here = min(G, nimg - n0);
+    const int cols = g_here * Pq;
+    const int m0 = blockIdx.y * (MT * 32);
+    const int Cin = G_.K;
+
+    // zero every staged plane once: the borders (ONNX padding) are never written again
+    for (int i = tid; i < IFKC * G * plane; i += 256) sIn[i] = 0.f;
+    // depthwise role: column dq (image g, position q), all IFKC channels of each chunk
+    const int dq = min(tid, cols - 1);
+    const int dg = dq / Pq, dqq = dq - dg * Pq;
+    const int oy = dqq / OW, ox = dqq - oy * OW;
+    const int lb = dg * plane + (oy * S) * Wp + ox * S;  // staged index of tap (0, 0)
+    const int pt = P.pad_t, pl = P.pad_l;
+    const float inv_W = 1.f / (float)W, inv_Pin = 1.f / (float)Pin;
+
+    f32x16 acc[MT][NTW];
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int u = 0; u < NTW; ++u)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
+
+    const int run = g_here * Pin;  // contiguous floats per channel for this tile
+    for (int kc = 0; kc < Cin; kc += IFKC) {
+        __syncthreads();  // previous chunk's readers are done with sIn / sW
+        // 1. copy the chunk's channel runs into the interiors of the padded planes
+        const int total = IFKC * run;
+        for (int base = 0; base < total; base += 256 * 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int e = min(base + tid + 256 * u, total - 1);
+                const int c = e / run, r = e - c * run;
+                const int ch = kc + c < Cin ? kc + c : Cin - 1;
+                v[u] = P.in.p[(size_t)(uint32_t)ch * (uint32_t)P.in.sC + (uint32_t)n0 * (uint32_t)P.in.sN + (uint32_t)r];
+                v[u] = kc + c < Cin ? v[u] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int e = base + tid + 256 * u;
+                if (e < total) {
+                    const int c = e / run, r = e - c * run;
+                    const int g = qdiv(r, Pin, inv_Pin), rr = r - g * Pin;
+                    const int iy = qdiv(rr, W, inv_W), ix = rr - iy * W;
+                    sIn[(c * G + g) * plane + (iy + pt) * Wp + ix + pl] = v[u];
+                }
+            }
+        }
+        for (int i = tid; i < IFKC * MT * 32; i += 256) {
+            const int r = i / (MT * 32), cc = i - r * (MT * 32);
+            const int k = kc + r, m = m0 + cc;
+            sW[i] = (k < Cin && m < G_.Mpad) ? G_.wt[(int64_t)k * G_.Mpad + m] : 0.f;
+        }
+        __syncthreads();
+        // 2. depthwise of all IFKC channels of this thread's column
+        float dv[IFKC];
+#pragma unroll
+        for (int c = 0; c < IFKC; ++c) {
+            const int cl = kc + c < Cin ? kc + c : Cin - 1;
+            const float *w = P.dw_w + cl * (K * K);
+            const float *t0 = sIn + c * G * plane + lb;
+            float a = P.dw_b[cl];
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx) a = __builtin_fmaf(w[ky * K + kx], t0[ky * Wp + kx], a);
+            dv[c] = a;
+        }
+        apply_act_n<IFKC>(P.dw_act, dv, [&](int c) { return kc + c < Cin ? kc + c : Cin - 1; });
+#pragma unroll
+        for (int c = 0; c < IFKC; ++c) sD[c * IBN + tid] = (kc + c < Cin && tid < cols) ? dv[c] : 0.f;
+        __syncthreads();
+        // 3. the 1x1 conv over the chunk
+#pragma unroll
+        for (int s = 0; s < IFKC / 2; ++s) {
+            float a[MT], b[NTW];
+#pragma unroll
+            for (int t = 0; t < MT; ++t) a[t] = sW[(2 * s + kh) * (MT * 32) + t * 32 + col];
+#pragma unroll
+            for (int u = 0; u < NTW; ++u) b[u] = sD[(2 * s + kh) * IBN + (wave * NTW + u) * 32 + col];
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+#pragma unroll
+                for (int u = 0; u < NTW; ++u)
+                    acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t], b[u], acc[t][u], 0, 0, 0);
+        }
+    }
+
+#pragma unroll
+    for (int u = 0; u < NTW; ++u) {
+        const int c = (wave * NTW + u) * 32 + col;
+        if (c >= cols) continue;
+        const int g = c / Pq, q = c - g * Pq;
+#pragma unroll
+        for (int t = 0; t < MT; ++t) epilogue_tile(G_, acc[t][u], n0 + g, q, m0 + t * 32, kh);
+    }
 }
 
 bool dwpw_supported(int k, int stride) { return (k == 3 || k == 5) && (stride == 1 || stride == 2); }
@@ -607,14 +730,57 @@ const char *dwpw_valu_co(const DwPwParams &p, hipStream_t s) {
 
 }  // namespace
 
+template <int K, int S, int MT>
+const char *dwpw_img_go(const DwPwParams &p, hipStream_t s) {
+    constexpr int NTW = IBN / 128;  // 4 waves x NTW x 32 = IBN columns
+    const int P = p.g.P, nimg = p.g.ncols / P, G = std::max(1, IBN / P);
+    const int ntiles = (nimg + G - 1) / G, mb = (p.g.Mpad + MT * 32 - 1) / (MT * 32);
+    const int Hp = (P / p.OW - 1) * S + K, Wp = (p.OW - 1) * S + K;
+    const size_t lds = sizeof(float) * ((size_t)IFKC * G * Hp * Wp + IFKC * IBN + IFKC * MT * 32);
+    dim3 grid((ntiles + 7) / 8 * 8, mb);
+    hipLaunchKernelGGL((dwpw_img_kernel<K, S, MT, NTW>), grid, dim3(256), lds, s, p, G, ntiles, nimg);
+    static char names[2][2][5][48];
+    char *nm = names[K == 5][S == 2][MT];
+    if (!nm[0]) snprintf(nm, 48, "dwpw_img_kernel<%d,%d,%d,%d>", K, S, MT, NTW);
+    return nm;
+}
+
+template <int K, int S>
+const char *dwpw_img_mt(const DwPwParams &p, hipStream_t s) {
+    switch (std::min(4, p.g.Mpad / 32)) {
+    case 1: return dwpw_img_go<K, S, 1>(p, s);
+    case 2: return dwpw_img_go<K, S, 2>(p, s);
+    case 3: return dwpw_img_go<K, S, 3>(p, s);
+    default: return dwpw_img_go<K, S, 4>(p, s);
+    }
+}
+
+// The image-tile form applies to planes of <= IBN positions whose padded staging fits in
+// 96 KiB (the depthwise input plane must be exactly the output plane's receptive area).
+static bool img_form(const DwPwParams &p) {
+    static const int mode = [] {  // opt-in (ZR_DWPW_IMG=1): slower than dwpw_kernel so far
+        const char *e = std::getenv("ZR_DWPW_IMG");
+        return e ? std::atoi(e) : 0;
+    }();
+    const int P = p.g.P;
+    // the tile's images must be one contiguous run per channel (CNHW activations)
+    if (!mode || P > IBN || p.g.ncols % P != 0 || P % p.OW != 0 || p.in.sN != (int64_t)p.in.H * p.in.W)
+        return false;
+    const int OH = P / p.OW, Hp = (OH - 1) * p.stride + p.k, Wp = (p.OW - 1) * p.stride + p.k;
+    // every input pixel must land inside the padded plane (no cropping)
+    if (p.pad_t + p.in.H > Hp || p.pad_l + p.in.W > Wp) return false;
+    const int G = std::max(1, IBN / P);
+    return sizeof(float) * ((size_t)IFKC * G * Hp * Wp + IFKC * IBN + IFKC * 128) <= 96 * 1024;
+}
+
 // The VALU form applies to (see dwpw_valu_kernel): >= 256 positions per image, W % 4 == 0
-// (16-byte row loads), Cout <= 64, Cin * Cout <= 1600, staged rows within 64 KiB.
+// (16-byte row loads), Cout <= 48, Cin * Cout <= 2048, staged rows within 64 KiB.
 static bool valu_form(const DwPwParams &p) {
     static const int mode = [] {  // ZR_DWPW_VALU=0 disables the form (A/B runs)
         const char *e = std::getenv("ZR_DWPW_VALU");
         return e ? std::atoi(e) : 1;
     }();
-    if (!mode || p.g.P < VTQ || p.in.W % 4 != 0 || p.g.M > 64 || p.g.K * p.g.M > 1600) return false;
+    if (!mode || p.g.P < VTQ || p.in.W % 4 != 0 || p.g.M > 48 || p.g.K * p.g.M > 2048) return false;
     if (p.g.ncols % p.g.P != 0) return false;
     const int rows = (VTQ / p.OW + 2) * p.stride + p.k;
     return sizeof(float) * (size_t)VFKC * rows * (p.in.W + 8) <= 64 * 1024;
@@ -632,6 +798,10 @@ const char *launch_dwpw(const DwPwParams &p, hipStream_t s) {
     if (valu_form(p)) {
         if (p.k == 3) return p.stride == 1 ? dwpw_valu_co<3, 1>(p, s) : dwpw_valu_co<3, 2>(p, s);
         return p.stride == 1 ? dwpw_valu_co<5, 1>(p, s) : dwpw_valu_co<5, 2>(p, s);
+    }
+    if (img_form(p)) {
+        if (p.k == 3) return p.stride == 1 ? dwpw_img_mt<3, 1>(p, s) : dwpw_img_mt<3, 2>(p, s);
+        return p.stride == 1 ? dwpw_img_mt<5, 1>(p, s) : dwpw_img_mt<5, 2>(p, s);
     }
     const int Wp = (p.OW - 1) * p.stride + p.k;
     if (rows_on && p.g.P >= RBN && p.g.Mpad <= 96 && Wp <= 128 && p.g.ncols % p.g.P == 0) {

@@ -203,6 +203,11 @@ struct CtxLock {
 int enqueue(zr_session *s, Ctx *c, int N, const float *input, int64_t in_sN, int64_t in_sC,
             float *const *outs, hipStream_t stream, const zr::PreprocParams *pre = nullptr) {
     const size_t need = (size_t)s->plan.arena_per_image * (size_t)N;
+    // kernels address every tensor with 32-bit element offsets (kernels/epilogue.h)
+    size_t largest = std::max(need, (size_t)(input ? in_sN : 0) * (size_t)N);
+    for (const auto &o : s->plan.outputs) largest = std::max(largest, (size_t)o.per_image * (size_t)N);
+    if (largest >= ((size_t)1 << 31))
+        return set_err(ZR_ERR_INVALID_ARGUMENT, "batch too large: a tensor would exceed 2^31 elements; split it");
     if (int rc = grow(c->arena, c->arena_floats, need ? need : 1)) return rc;
     HIP_TRY(hipStreamWaitEvent(stream, c->done, 0));
     zr::Binding b;
