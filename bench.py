@@ -61,6 +61,36 @@ def kernel_symbol(name: str) -> str:
     return name.replace(" ", "")
 
 
+def roofline_of(kernels, traffic):
+    """Roofline of the dominant kernel symbol (most total time; one symbol may serve both
+    networks, so records aggregate by symbol): algorithmic bytes (or FLOPs) per launch over
+    its average HIP-event launch duration, against HBM or f32-MFMA peak."""
+    by_symbol = {}
+    for k in kernels:
+        sym = k["kernel"].split("/", 1)[-1]
+        a = by_symbol.setdefault(sym, {"kernel": sym, "launches": 0, "ms": 0.0, "bytes": 0.0, "flops": 0.0})
+        for f in ("launches", "ms", "bytes", "flops"):
+            a[f] += k[f]
+    if not by_symbol:
+        return None
+    dom = max(by_symbol.values(), key=lambda k: k["ms"])
+    avg_s = dom["ms"] / dom["launches"] / 1e3
+    gbs = dom["bytes"] / dom["launches"] / avg_s / 1e9
+    tfl = dom["flops"] / dom["launches"] / avg_s / 1e12
+    if tfl / FP32_PEAK_TFLOPS > gbs / HBM_PEAK_GBS:
+        r = {"bound": "mfma", "achieved": round(tfl, 3), "peak": FP32_PEAK_TFLOPS,
+             "unit": "TFLOP/s", "frac": round(tfl / FP32_PEAK_TFLOPS, 4)}
+    else:
+        r = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+             "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    r["traffic"] = round(traffic[dom["kernel"]]) if traffic and dom["kernel"] in traffic else None
+    r["kernel"] = dom["kernel"]
+    r["avg_launch_us"] = round(avg_s * 1e6, 2)
+    r["algorithmic_bytes_per_launch"] = round(dom["bytes"] / dom["launches"])
+    r["kernel_share"] = round(dom["ms"] / sum(k["ms"] for k in kernels), 3)
+    return r
+
+
 def measure_traffic(args):
     """HBM bytes per launch of every kernel symbol, from two rocprofv3 --pmc passes (one counter
     each, no other trace domain) over a short child run of this same benchmark.  Per
@@ -294,30 +324,29 @@ def main():
         if traffic and sym in traffic:
             k["traffic_per_launch_symbol_avg"] = round(traffic[sym])
         kernels.append(k)
-    roofline = None
-    by_symbol = {}
-    for k in kernels:  # one kernel symbol may serve both networks: aggregate by symbol
-        sym = k["kernel"].split("/", 1)[-1]
-        a = by_symbol.setdefault(sym, {"kernel": sym, "launches": 0, "ms": 0.0, "bytes": 0.0, "flops": 0.0})
-        for f in ("launches", "ms", "bytes", "flops"):
-            a[f] += k[f]
-    if by_symbol:
-        dom = max(by_symbol.values(), key=lambda k: k["ms"])
-        avg_s = dom["ms"] / dom["launches"] / 1e3
-        gbs = dom["bytes"] / dom["launches"] / avg_s / 1e9
-        tfl = dom["flops"] / dom["launches"] / avg_s / 1e12
-        if tfl / FP32_PEAK_TFLOPS > gbs / HBM_PEAK_GBS:
-            roofline = {"bound": "mfma", "achieved": round(tfl, 3), "peak": FP32_PEAK_TFLOPS,
-                        "unit": "TFLOP/s", "frac": round(tfl / FP32_PEAK_TFLOPS, 4)}
-        else:
-            roofline = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
-        roofline["traffic"] = round(traffic[dom["kernel"]]) if traffic and dom["kernel"] in traffic else None
-        roofline["kernel"] = dom["kernel"]
-        roofline["avg_launch_us"] = round(avg_s * 1e6, 2)
-        roofline["algorithmic_bytes_per_launch"] = round(dom["bytes"] / dom["launches"])
-        total_ms = sum(k["ms"] for k in kernels)
-        roofline["kernel_share"] = round(dom["ms"] / total_ms, 3)
+    roofline = roofline_of(kernels, traffic)
+    # The timed region runs the sub-batches on concurrent streams, so a launch shares the GPU
+    # with the other stream's kernels and its HIP-event duration overstates the kernel's own.
+    # The same frames once more on ONE stream give each kernel's uncontended launch time.
+    roofline_isolated = None
+    if not args.no_profile and world == 1:
+        pipe1 = H.DetectTrackPipeline(args.workload, device, args.threads,
+                                      1 if args.workload == "face" else 4, args.sub_batches, False)
+        pipe1.set_frames(flist, forced)
+        for _ in range(2):
+            pipe1.run_frames()
+        pipe1.profile_read()
+        pipe1.profile(True)
+        for _ in range(max(3, args.steps // 2)):
+            pipe1.run_frames()
+        iso = []
+        for line in pipe1.profile_read().splitlines():
+            name, n, ms, by, fl = line.rsplit(" ", 4)
+            iso.append({"kernel": name, "launches": int(n), "ms": float(ms), "bytes": float(by), "flops": float(fl)})
+        pipe1.profile(False)
+        roofline_isolated = roofline_of(iso, traffic)
+        if roofline_isolated:
+            roofline_isolated["note"] = "same frames, sub-batches on one HIP stream (no cross-stream overlap)"
     st = pipe.stats()
     frames_per_s = world * B * args.steps / elapsed
     bytes_frame = st["detector_bytes_per_image"] + st["landmarker_bytes_per_image"] * faces / (B * args.steps)
@@ -353,6 +382,7 @@ def main():
         "stage_ms_per_step": {k: round(v / args.steps, 3) for k, v in stage.items()},
         "pipeline_algorithmic_GBs_per_gpu": round(pipeline_gbs_per_gpu, 1),
         "roofline": roofline,
+        "roofline_isolated": roofline_isolated,
         "kernels": sorted(kernels, key=lambda k: -k["ms"]),
         "cpu_baseline": cpu,
     }

@@ -196,8 +196,12 @@ __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) 
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
 
-    for (int kc = 0; kc < Cin; kc += FKC) {
-        float tap[PER][KK];
+    // Software pipeline over the channel chunks: the taps and 1x1 weights of chunk k+1 are
+    // loaded into registers while the waves run chunk k's MFMAs, so the global-load latency of
+    // every chunk after the first hides behind matrix work.
+    constexpr int WPT = (FKC * BM + 255) / 256;  // 1x1 weights staged per thread per chunk
+    float tap[PER][KK], wreg[WPT];
+    auto load_chunk = [&](int kc) {
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int c = kc + dc + CPAR * i;
@@ -205,6 +209,17 @@ __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) 
 #pragma unroll
             for (int t = 0; t < KK; ++t) tap[i][t] = *(const float *)(pl + off[t]);
         }
+#pragma unroll
+        for (int u = 0; u < WPT; ++u) {
+            const int i = min(tid + 256 * u, FKC * BM - 1);
+            const int r = i / BM, cc = i - r * BM;
+            const int k = kc + r, m = m0 + cc;
+            const float x = G.wt[(int64_t)(k < Cin ? k : Cin - 1) * G.Mpad + (m < G.Mpad ? m : 0)];
+            wreg[u] = (k < Cin && m < G.Mpad) ? x : 0.f;
+        }
+    };
+    load_chunk(0);
+    for (int kc = 0; kc < Cin; kc += FKC) {
         float dv[PER];
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
@@ -222,12 +237,13 @@ __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) 
         });
 #pragma unroll
         for (int i = 0; i < PER; ++i) sD[dc + CPAR * i][dj] = kc + dc + CPAR * i < Cin ? dv[i] : 0.f;
-        for (int i = tid; i < FKC * BM; i += 256) {
-            const int r = i / BM, cc = i - r * BM;
-            const int k = kc + r, m = m0 + cc;
-            sW[r][cc] = (k < Cin && m < G.Mpad) ? G.wt[(int64_t)k * G.Mpad + m] : 0.f;
+#pragma unroll
+        for (int u = 0; u < WPT; ++u) {
+            const int i = tid + 256 * u;
+            if (i < FKC * BM) (&sW[0][0])[i] = wreg[u];
         }
         __syncthreads();
+        if (kc + FKC < Cin) load_chunk(kc + FKC);
 #pragma unroll
         for (int s = 0; s < FKC / 2; ++s) {
             float a[MTW], b[NTW];
