@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--sub-batches", type=int, default=2)
     ap.add_argument("--streams", choices=["multi", "single"], default="multi")
+    ap.add_argument("--no-cross-step", action="store_true",
+                    help="one pipeline call per step (no overlap across step boundaries)")
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the rocprofv3 FETCH_SIZE/WRITE_SIZE passes behind roofline.traffic")
     return ap.parse_args()
@@ -275,8 +277,15 @@ def main():
             shard.all_gather_records(gather_in)
         return pipe.num_rois()
 
-    for _ in range(args.warmup):
-        step()
+    # N = 1: the steps run back to back in one call that overlaps each step's host tail
+    # (landmark mapping) with the next step's detection on the GPU (run_frames_repeated).
+    # N > 1 keeps one call per step: every step ends in the all-gather of its detections.
+    repeated = world == 1 and not args.no_cross_step
+    if repeated:
+        pipe.run_frames_repeated(args.warmup)
+    else:
+        for _ in range(args.warmup):
+            step()
     if not args.no_profile:
         pipe.profile_read()  # drop warmup records
         pipe.profile(True)
@@ -287,12 +296,19 @@ def main():
     faces = 0
     stage = {"detect_gpu_ms": 0.0, "decode_nms_ms": 0.0, "landmark_gpu_ms": 0.0, "map_ms": 0.0}
     dets_total = 0
-    for _ in range(args.steps):
-        faces += step()
+    if repeated:
+        faces = pipe.run_frames_repeated(args.steps)
         t = pipe.times()
         for k in stage:
-            stage[k] += t[k]
-        dets_total += t["detections"]
+            stage[k] = t[k]
+        dets_total = t["detections"]
+    else:
+        for _ in range(args.steps):
+            faces += step()
+            t = pipe.times()
+            for k in stage:
+                stage[k] += t[k]
+            dets_total += t["detections"]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -333,12 +349,10 @@ def main():
         pipe1 = H.DetectTrackPipeline(args.workload, device, args.threads,
                                       1 if args.workload == "face" else 4, args.sub_batches, False)
         pipe1.set_frames(flist, forced)
-        for _ in range(2):
-            pipe1.run_frames()
+        pipe1.run_frames_repeated(2)
         pipe1.profile_read()
         pipe1.profile(True)
-        for _ in range(max(3, args.steps // 2)):
-            pipe1.run_frames()
+        pipe1.run_frames_repeated(max(3, args.steps // 2))
         iso = []
         for line in pipe1.profile_read().splitlines():
             name, n, ms, by, fl = line.rsplit(" ", 4)

@@ -116,3 +116,27 @@ def test_pipeline_equals_per_frame_api(H, kind):
         if res is not None:
             assert np.array_equal(res["landmarks"], r["landmarks"])
             assert res["updated_roi"].rect() == r["updated_roi"].rect()
+
+
+def test_repeated_runs_equal_single_run(H):
+    """run_frames_repeated overlaps one run's landmark mapping with the next run's detection;
+    each run must still produce exactly what one run_frames() produces."""
+    from zaru_amd._lib import DeviceBuffer
+    rng = np.random.default_rng(31)
+    frames = [rng.integers(0, 256, size=(360, 640, 4), dtype=np.uint8) for _ in range(6)]
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "sad_linus_face.npz"))
+    frames[1][:128, :128, :3] = g["codes"].transpose(1, 2, 0)
+    bufs = [DeviceBuffer.from_array(f) for f in frames]
+    flist = [(b.ptr, f.shape[1], f.shape[0], f.shape[1] * 4) for b, f in zip(bufs, frames)]
+    forced = [[(320.0, 180.0, 160.0, 160.0, 0.0)] for _ in frames]
+    p = H.DetectTrackPipeline("face", 0, 4, 4, 3)
+    p.set_frames(flist, forced)
+    n1 = p.run_frames()
+    want = [(r["frame"], r["landmarks"].copy(), r["tracked"]) for r in (p.roi(i) for i in range(n1))]
+    want_det = [[(d.confidence(), d.bounding_rect().tuple()) for d in ds] for ds in p.detections()]
+    total = p.run_frames_repeated(3)
+    assert total == 3 * n1 and p.num_rois() == n1
+    for i, (f, lm, tr) in enumerate(want):
+        r = p.roi(i)
+        assert r["frame"] == f and r["tracked"] == tr and np.array_equal(r["landmarks"], lm)
+    assert [[(d.confidence(), d.bounding_rect().tuple()) for d in ds] for ds in p.detections()] == want_det

@@ -331,6 +331,11 @@ PYBIND11_MODULE(_zaru_host, m) {
             p.run_frames();
             return p.rois().size();
         })
+        .def("run_frames_repeated", [](DetectTrackPipeline &p, int steps) {
+            py::gil_scoped_release nogil;
+            p.run_frames_repeated(steps);
+            return p.times().rois;
+        }, py::arg("steps"))
         .def("detections", [](const DetectTrackPipeline &p) { return p.detections(); })
         .def("detection_records", [](const DetectTrackPipeline &p, uint32_t rmax, uint32_t first_id,
                                      uint32_t id_stride) {

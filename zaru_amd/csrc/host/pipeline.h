@@ -97,6 +97,11 @@ class DetectTrackPipeline {
     // the same device frames pay no per-call argument conversion
     void set_frames(std::vector<Image> frames, std::vector<std::vector<RotatedRect>> forced);
     void run_frames() { run(frames_, forced_); }
+    // `steps` consecutive runs over the resident frames, software-pipelined across run
+    // boundaries: the next run's detections are enqueued behind this run's landmark launches,
+    // before this run's landmark mapping, so the GPU never waits for the host between runs.
+    // Results are the last run's; times() sums all runs.
+    void run_frames_repeated(int steps);
 
   private:
     // one software-pipeline slot: a contiguous range of frames with its own stream/buffers

@@ -796,7 +796,8 @@ static bool valu_form(const DwPwParams &p) {
         const char *e = std::getenv("ZR_DWPW_VALU");
         return e ? std::atoi(e) : 1;
     }();
-    if (!mode || p.g.P < VTQ || p.in.W % 4 != 0 || p.g.M > 48 || p.g.K * p.g.M > 2048) return false;
+    if (!mode || p.g.P < VTQ || p.in.W % 4 != 0 || p.in.W > 248 || p.g.M > 48 || p.g.K * p.g.M > 2048)
+        return false;
     if (p.g.ncols % p.g.P != 0) return false;
     const int rows = (VTQ / p.OW + 2) * p.stride + p.k;
     return sizeof(float) * (size_t)VFKC * rows * (p.in.W + 8) <= 64 * 1024;
