@@ -223,8 +223,11 @@ const char *launch_gemm(const GemmParams &p, hipStream_t s) {
     const bool rowmajor = p.KK == 1 && p.x_sN == p.P && (p.x_sC % 4) == 0 && (p.ncols % 4) == 0 &&
                           ((uintptr_t)p.x % 16) == 0 && (p.Mpad % 4) == 0 && ((uintptr_t)p.wt % 16) == 0;
     if (rowmajor) {
-        int mt = std::min(4, mtiles);
-        const int nt = p.ncols >= 256 * 256 ? 2 : 1;  // wide tiles once there are >= 256 of them
+        // K <= 64 (the expand convs): one or two K-chunks, so operand reuse buys nothing and
+        // the launch is bound by its output stores -- small tiles, high occupancy
+        const bool skinny = p.K <= 64;
+        int mt = std::min(skinny ? 1 : 4, mtiles);
+        const int nt = !skinny && p.ncols >= 256 * 256 ? 2 : 1;  // wide tiles once there are >= 256 of them
         const int bn = 4 * nt * 32;
         // keep >= ~2 workgroups per CU: trade M-tile reuse for parallelism on small problems
         while (mt > 1 && (int64_t)((p.ncols + bn - 1) / bn) * ((mtiles + mt - 1) / mt) < 512) --mt;
