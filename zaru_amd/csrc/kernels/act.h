@@ -4,11 +4,18 @@
 
 namespace zr {
 
+// Read-only parameters (weights, biases, slopes) through the constant address space: such loads
+// are invariant for the kernel, so uniform ones become scalar (s_load) loads even in kernels
+// that write LDS by DMA, and no vector-memory wait (which would also drain the DMA) guards them.
+__device__ __forceinline__ float ldc(const float *p, int i) {
+    return ((const __attribute__((address_space(4))) float *)p)[i];
+}
+
 __device__ __forceinline__ float apply_act(const Act &a, float v, int c) {
     switch (a.kind) {
     case ACT_RELU: return fmaxf(v, 0.f);
     case ACT_CLIP: return fminf(fmaxf(v, a.lo), a.hi);
-    case ACT_PRELU: return v < 0.f ? v * a.slope[c] : v;
+    case ACT_PRELU: return v < 0.f ? v * ldc(a.slope, c) : v;
     case ACT_SIGMOID: return 1.f / (1.f + expf(-v));
     default: return v;
     }
@@ -31,7 +38,7 @@ __device__ __forceinline__ void apply_act_n(const Act &a, float *v, ChanFn ch) {
     case ACT_PRELU: {
         float s[N];
 #pragma unroll
-        for (int r = 0; r < N; ++r) s[r] = a.slope[ch(r)];
+        for (int r = 0; r < N; ++r) s[r] = ldc(a.slope, ch(r));
 #pragma unroll
         for (int r = 0; r < N; ++r) v[r] = v[r] < 0.f ? v[r] * s[r] : v[r];
         break;

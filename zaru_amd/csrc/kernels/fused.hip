@@ -143,7 +143,13 @@ const char *launch_stem(const StemParams &p, bool pre, hipStream_t s) {
 // for the few-channel high-resolution layers, tall channel tiles for the 128/256-channel
 // low-resolution ones.  Column tiles are dealt to XCDs in contiguous runs, so halo rows and the
 // residual re-read are L2 hits on the XCD that just fetched them.
-template <int K, int S, int WM, int MTW, int NTW>
+// V4: the depthwise part computes 4 horizontally adjacent outputs per thread from one input
+// window per row (float4 loads plus pad_l scalars) instead of K*K lane-private taps per
+// output: ~4x fewer memory instructions.  Needs OW % 4 == 0, W % 4 == 0 and the models'
+// TF-style pads (K3: 1 for stride 1, 0 for stride 2; K5: 2 / 1) -- see v4_ok().
+template <int K, int S> struct DwPad { static constexpr int L = S == 1 ? K / 2 : K / 2 - 1; };
+
+template <int K, int S, int WM, int MTW, int NTW, bool V4>
 __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) {
     constexpr int WN = 4 / WM;
     constexpr int BN = WN * NTW * 32, BM = WM * MTW * 32;
@@ -152,7 +158,12 @@ __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) 
     constexpr int CPAR = 256 / BN;        // channels whose depthwise runs side by side
     constexpr int PER = FKC / CPAR;       // depthwise outputs per thread per chunk
     static_assert(PER >= 1 && FKC % CPAR == 0, "tile/chunk mismatch");
-    __shared__ float sD[FKC][BN];
+    // V4 layout: Q column quads x CS channel slots; CPT channels per thread
+    constexpr int Q = BN / 4, CS = 256 / Q, CPT = FKC > CS ? FKC / CS : 1;
+    constexpr int PL = DwPad<K, S>::L;
+    constexpr int NV = (3 * S + K - PL + 3) / 4;  // float4 loads per window row
+    constexpr int WL = PL + 4 * NV;               // window floats per row
+    __shared__ __attribute__((aligned(16))) float sD[FKC][BN];
     __shared__ float sW[FKC][BM];
     const GemmParams &G = P.g;
 
@@ -188,6 +199,14 @@ __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) 
             mask |= (ok ? 1u : 0u) << (ky * K + kx);
         }
 
+    // V4 role: column quad qd (positions j4 .. j4+3 of one image row), channel slot cs
+    const int qd = tid % Q, cs = tid / Q;
+    const int j4 = min(j0 + 4 * qd, G.ncols - 4);
+    const int n4 = j4 / G.P, q4 = j4 - n4 * G.P;
+    const int oy4 = q4 / P.OW, ox4 = q4 - oy4 * P.OW;
+    const int a4 = ox4 * S;  // 16-byte aligned window start (W % 4 == 0, ox4 % 4 == 0)
+    const uint32_t nbase4 = (uint32_t)n4 * (uint32_t)P.in.sN;
+
     f32x16 acc[MTW][NTW];
 #pragma unroll
     for (int t = 0; t < MTW; ++t)
@@ -200,14 +219,44 @@ __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) 
     // loaded into registers while the waves run chunk k's MFMAs, so the global-load latency of
     // every chunk after the first hides behind matrix work.
     constexpr int WPT = (FKC * BM + 255) / 256;  // 1x1 weights staged per thread per chunk
-    float tap[PER][KK], wreg[WPT];
+    float tap[V4 ? 1 : PER][V4 ? 1 : KK], win[V4 ? CPT : 1][V4 ? K : 1][V4 ? WL : 1], wreg[WPT];
     auto load_chunk = [&](int kc) {
+        if constexpr (V4) {
 #pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int c = kc + dc + CPAR * i;
-            const char *pl = (const char *)(P.in.p + (size_t)(uint32_t)(c < Cin ? c : Cin - 1) * (uint32_t)P.in.sC);
+            for (int i = 0; i < CPT; ++i) {
+                const int c = kc + cs + CS * i;
+                const float *pl = P.in.p + (size_t)(uint32_t)(c < Cin ? c : Cin - 1) * (uint32_t)P.in.sC + nbase4;
 #pragma unroll
-            for (int t = 0; t < KK; ++t) tap[i][t] = *(const float *)(pl + off[t]);
+                for (int ky = 0; ky < K; ++ky) {
+                    const int iy = oy4 * S - P.pad_t + ky;
+                    const bool rok = iy >= 0 && iy < H;
+                    const uint32_t rb = (uint32_t)(rok ? iy : 0) * (uint32_t)W;
+#pragma unroll
+                    for (int e = 0; e < PL; ++e) {  // left of the aligned part
+                        const int x = a4 - PL + e;
+                        const float v = pl[rb + (uint32_t)(x >= 0 ? x : 0)];
+                        win[i][ky][e] = rok && x >= 0 ? v : 0.f;
+                    }
+#pragma unroll
+                    for (int v4 = 0; v4 < NV; ++v4) {
+                        const int x = a4 + 4 * v4;
+                        const bool ok = rok && x < W;
+                        const float4 v = *(const float4 *)(pl + rb + (uint32_t)(ok ? x : 0));
+                        win[i][ky][PL + 4 * v4 + 0] = ok ? v.x : 0.f;
+                        win[i][ky][PL + 4 * v4 + 1] = ok ? v.y : 0.f;
+                        win[i][ky][PL + 4 * v4 + 2] = ok ? v.z : 0.f;
+                        win[i][ky][PL + 4 * v4 + 3] = ok ? v.w : 0.f;
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int c = kc + dc + CPAR * i;
+                const char *pl = (const char *)(P.in.p + (size_t)(uint32_t)(c < Cin ? c : Cin - 1) * (uint32_t)P.in.sC);
+#pragma unroll
+                for (int t = 0; t < KK; ++t) tap[i][t] = *(const float *)(pl + off[t]);
+            }
         }
 #pragma unroll
         for (int u = 0; u < WPT; ++u) {
@@ -220,23 +269,56 @@ __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) 
     };
     load_chunk(0);
     for (int kc = 0; kc < Cin; kc += FKC) {
-        float dv[PER];
+        if constexpr (V4) {
+            float dv[CPT * 4];
 #pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int c = kc + dc + CPAR * i;
-            const int cl = c < Cin ? c : Cin - 1;
-            const float *w = P.dw_w + cl * KK;
-            float a = P.dw_b[cl];
+            for (int i = 0; i < CPT; ++i) {
+                const int c = kc + cs + CS * i;
+                const int cl = c < Cin ? c : Cin - 1;
+                const float *w = P.dw_w + cl * KK;
+                const float b = P.dw_b[cl];
 #pragma unroll
-            for (int t = 0; t < KK; ++t) a = __builtin_fmaf(w[t], ((mask >> t) & 1u) ? tap[i][t] : 0.f, a);
-            dv[i] = a;
+                for (int o = 0; o < 4; ++o) {
+                    float a = b;
+#pragma unroll
+                    for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+                        for (int kx = 0; kx < K; ++kx) a = __builtin_fmaf(w[ky * K + kx], win[i][ky][o * S + kx], a);
+                    dv[4 * i + o] = a;
+                }
+            }
+            apply_act_n<CPT * 4>(P.dw_act, dv, [&](int e) {
+                const int c = kc + cs + CS * (e >> 2);
+                return c < Cin ? c : Cin - 1;
+            });
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int c = cs + CS * i;
+                if (c < FKC) {
+                    const bool ok = kc + c < Cin;
+                    *(float4 *)&sD[c][4 * qd] = make_float4(ok ? dv[4 * i] : 0.f, ok ? dv[4 * i + 1] : 0.f,
+                                                            ok ? dv[4 * i + 2] : 0.f, ok ? dv[4 * i + 3] : 0.f);
+                }
+            }
+        } else {
+            float dv[PER];
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int c = kc + dc + CPAR * i;
+                const int cl = c < Cin ? c : Cin - 1;
+                const float *w = P.dw_w + cl * KK;
+                float a = P.dw_b[cl];
+#pragma unroll
+                for (int t = 0; t < KK; ++t) a = __builtin_fmaf(w[t], ((mask >> t) & 1u) ? tap[i][t] : 0.f, a);
+                dv[i] = a;
+            }
+            apply_act_n<PER>(P.dw_act, dv, [&](int i) {
+                const int c = kc + dc + CPAR * i;
+                return c < Cin ? c : Cin - 1;
+            });
+#pragma unroll
+            for (int i = 0; i < PER; ++i) sD[dc + CPAR * i][dj] = kc + dc + CPAR * i < Cin ? dv[i] : 0.f;
         }
-        apply_act_n<PER>(P.dw_act, dv, [&](int i) {
-            const int c = kc + dc + CPAR * i;
-            return c < Cin ? c : Cin - 1;
-        });
-#pragma unroll
-        for (int i = 0; i < PER; ++i) sD[dc + CPAR * i][dj] = kc + dc + CPAR * i < Cin ? dv[i] : 0.f;
 #pragma unroll
         for (int u = 0; u < WPT; ++u) {
             const int i = tid + 256 * u;
@@ -415,8 +497,14 @@ __device__ __forceinline__ int qdiv(int a, int b, float inv_b) {
     return q;
 }
 
-template <int K, int S, int CO>
-__global__ __launch_bounds__(256) void dwpw_valu_kernel(const DwPwParams P, int tpi, int ntiles, int rmax, int lw) {
+__device__ const float4 zr_zero4 = {0.f, 0.f, 0.f, 0.f};  // LDS-DMA source of the zero slots
+
+// DB: the staging goes global -> LDS by LDS-DMA (global_load_lds_dwordx4) into two buffers, the
+// next chunk's copy in flight while the current chunk is computed (one barrier per chunk).  The
+// staged image is slot-linear (slot = 16 B; row stride lw = 4 * srow floats), exactly the
+// lane-linear order one DMA wave-instruction writes; zero slots (padding) read zr_zero4.
+template <int K, int S, int CO, bool DB>
+__global__ __launch_bounds__(256) void dwpw_valu_kernel(const DwPwParams P, int tpi, int ntiles, int bufsz, int lw) {
     extern __shared__ __attribute__((aligned(16))) float sIn[];  // [VFKC * rows][lw]
     const GemmParams &G = P.g;
     const int cpx = gridDim.x >> 3;  // gridDim.x is a multiple of 8
@@ -427,7 +515,7 @@ __global__ __launch_bounds__(256) void dwpw_valu_kernel(const DwPwParams P, int 
     const int Pq = G.P, H = P.in.H, W = P.in.W, Cin = G.K, OW = P.OW;
     const int oy_a = q0 / OW, oy_b = min(q0 + VTQ - 1, Pq - 1) / OW;
     const int iy_a = oy_a * S - P.pad_t;
-    const int R = (oy_b - oy_a) * S + K;  // <= rmax
+    const int R = (oy_b - oy_a) * S + K;  // VFKC * R * lw <= bufsz (floats per LDS buffer)
     const int q = min(q0 + tid, Pq - 1);
     const int oy = q / OW, ox = q - oy * OW;
     // LDS row layout: 4 zero floats, the W input values, >= 4 zero floats (lw % 4 == 0)
@@ -440,8 +528,30 @@ __global__ __launch_bounds__(256) void dwpw_valu_kernel(const DwPwParams P, int 
 #pragma unroll
     for (int i = 0; i < CO / 2; ++i) acc[i] = (f32x2)(0.f);
 
-    for (int kc = 0; kc < Cin; kc += VFKC) {
-        const int total = VFKC * R * srow;
+    const int total = VFKC * R * srow;
+    auto stage_dma = [&](int kc, float *dst) {
+        const int nwi = (total + 63) >> 6, lane = tid & 63;
+        for (int wi = tid >> 6; wi < nwi; wi += 4) {
+            const int sl = wi * 64 + lane;
+            const int cr = qdiv(sl, srow, inv_srow), sx = sl - cr * srow;
+            const int c = qdiv(cr, R, inv_R), r = cr - c * R;
+            const int iy = iy_a + r, ch = kc + c, xv = sx - 1;
+            const bool ok = sl < total && iy >= 0 && iy < H && ch < Cin && xv >= 0 && 4 * xv < W;
+            const float *src = ok ? P.in.p + (size_t)(uint32_t)ch * (uint32_t)P.in.sC + nbase + (uint32_t)(iy * W + 4 * xv)
+                                  : (const float *)&zr_zero4;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                             (__attribute__((address_space(3))) void *)(dst + wi * 256), 16, 0, 0);
+        }
+    };
+    if constexpr (DB) stage_dma(0, sIn);
+
+    for (int kc = 0, it = 0; kc < Cin; kc += VFKC, ++it) {
+        const float *buf = sIn;
+        if constexpr (DB) {
+            buf = sIn + (it & 1) * bufsz;
+            __syncthreads();  // vmcnt(0) + barrier: chunk kc has landed, chunk kc - VFKC's readers are done
+            if (kc + VFKC < Cin) stage_dma(kc + VFKC, sIn + ((it + 1) & 1) * bufsz);
+        } else
         for (int base = 0; base < total; base += 1024) {
             float4 v[4];
 #pragma unroll
@@ -464,24 +574,25 @@ __global__ __launch_bounds__(256) void dwpw_valu_kernel(const DwPwParams P, int 
                 }
             }
         }
-        __syncthreads();
+        if constexpr (!DB) __syncthreads();
 #pragma unroll 2
         for (int c = 0; c < VFKC; ++c) {
             const int ch = kc + c;
             if (ch >= Cin) break;
-            const float *t0 = sIn + c * R * lw + lb;
+            const float *t0 = buf + c * R * lw + lb;
             const float *w = P.dw_w + ch * (K * K);
-            float d = P.dw_b[ch];
+            float d = ldc(P.dw_b, ch);
 #pragma unroll
             for (int ky = 0; ky < K; ++ky)
 #pragma unroll
-                for (int kx = 0; kx < K; ++kx) d = __builtin_fmaf(w[ky * K + kx], t0[ky * lw + kx], d);
+                for (int kx = 0; kx < K; ++kx) d = __builtin_fmaf(ldc(w, ky * K + kx), t0[ky * lw + kx], d);
             d = apply_act(P.dw_act, d, ch);
-            const f32x2 *w2 = (const f32x2 *)(G.wt + (size_t)ch * G.Mpad);  // [Kpad][Mpad]
+            const __attribute__((address_space(4))) f32x2 *w2 =
+                (const __attribute__((address_space(4))) f32x2 *)(G.wt + (size_t)ch * G.Mpad);  // [Kpad][Mpad]
 #pragma unroll
             for (int i = 0; i < CO / 2; ++i) acc[i] = __builtin_elementwise_fma(w2[i], (f32x2)(d), acc[i]);
         }
-        __syncthreads();
+        if constexpr (!DB) __syncthreads();
     }
 
     if (q0 + tid >= Pq) return;
@@ -658,16 +769,30 @@ struct DwPwLayout {
 constexpr DwPwLayout kLayouts[] = {{1, 1, 1}, {1, 2, 1}, {1, 3, 1}, {1, 4, 1}, {2, 1, 1},
                                    {2, 2, 1}, {2, 4, 1}, {4, 1, 1}, {4, 2, 1}};
 
+// The V4 depthwise form (see dwpw_kernel) applies when rows split into aligned quads and the
+// layer uses the models' TF-style pads.
+static bool v4_ok(const DwPwParams &p) {
+    static const int mode = [] {  // ZR_DWPW_V4=0 disables the form (A/B runs)
+        const char *e = std::getenv("ZR_DWPW_V4");
+        return e ? std::atoi(e) : 1;
+    }();
+    const int pl = p.stride == 1 ? p.k / 2 : p.k / 2 - 1;
+    return mode && p.OW % 4 == 0 && p.in.W % 4 == 0 && p.pad_l == pl && p.pad_t == pl &&
+           p.g.ncols % 4 == 0 && p.g.P % 4 == 0;
+}
+
 template <int K, int S, int WM, int MTW>
 const char *dwpw_go(const DwPwParams &p, hipStream_t s) {
     constexpr int BN = (4 / WM) * 32, BM = WM * MTW * 32;
     const int nct = (p.g.ncols + BN - 1) / BN;
     const int mb = (p.g.Mpad + BM - 1) / BM;
     dim3 grid((nct + 7) / 8 * 8, mb);
-    hipLaunchKernelGGL((dwpw_kernel<K, S, WM, MTW, 1>), grid, dim3(256), 0, s, p, nct);
-    static char names[2][2][5][5][40];  // the symbol as rocprofv3 prints it, spaces removed
-    char *nm = names[K == 5][S == 2][WM][MTW];
-    if (!nm[0]) snprintf(nm, 40, "dwpw_kernel<%d,%d,%d,%d,1>", K, S, WM, MTW);
+    const bool v4 = v4_ok(p);
+    if (v4) hipLaunchKernelGGL((dwpw_kernel<K, S, WM, MTW, 1, true>), grid, dim3(256), 0, s, p, nct);
+    else hipLaunchKernelGGL((dwpw_kernel<K, S, WM, MTW, 1, false>), grid, dim3(256), 0, s, p, nct);
+    static char names[2][2][5][5][2][48];  // the symbol as rocprofv3 prints it, spaces removed
+    char *nm = names[K == 5][S == 2][WM][MTW][v4];
+    if (!nm[0]) snprintf(nm, 48, "dwpw_kernel<%d,%d,%d,%d,1,%s>", K, S, WM, MTW, v4 ? "true" : "false");
     return nm;
 }
 
@@ -727,12 +852,27 @@ const char *dwpw_valu_go(const DwPwParams &p, hipStream_t s) {
         rmax = std::max(rmax, (b - a) * S + K);
     }
     const int lw = p.in.W + 8;
-    const size_t lds = sizeof(float) * (size_t)VFKC * rmax * lw;
+    // double-buffered LDS-DMA staging for the 32-channel outputs, whose 131 VGPRs hold a CU to
+    // 3 workgroups anyway (two buffers of <= 32 KiB keep that); at 16 channels 5 workgroups fit
+    // by registers and the second buffer would cost occupancy, at 48 it measured slower.
+    // ZR_VALU_DB=0 disables it (A/B runs), 2 allows it for every CO.
+    static const int db_mode = [] {
+        const char *e = std::getenv("ZR_VALU_DB");
+        return e ? std::atoi(e) : 1;
+    }();
+    const int bufsz = (VFKC * rmax * lw + 255) / 256 * 256;  // whole 1 KiB DMA wave-instructions
+    const bool db = db_mode && (CO == 32 || db_mode == 2) && 2 * sizeof(float) * (size_t)bufsz <= 64 * 1024;
     dim3 grid((ntiles + 7) / 8 * 8);
-    hipLaunchKernelGGL((dwpw_valu_kernel<K, S, CO>), grid, dim3(256), lds, s, p, tpi, ntiles, rmax, lw);
-    static char names[2][2][5][48];
-    char *nm = names[K == 5][S == 2][CO / 16];
-    if (!nm[0]) snprintf(nm, 48, "dwpw_valu_kernel<%d,%d,%d>", K, S, CO);
+    if (db) {
+        const size_t lds = 2 * sizeof(float) * (size_t)bufsz;
+        hipLaunchKernelGGL((dwpw_valu_kernel<K, S, CO, true>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
+    } else {
+        const size_t lds = sizeof(float) * (size_t)VFKC * rmax * lw;
+        hipLaunchKernelGGL((dwpw_valu_kernel<K, S, CO, false>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
+    }
+    static char names[2][2][5][2][56];
+    char *nm = names[K == 5][S == 2][CO / 16][db];
+    if (!nm[0]) snprintf(nm, 56, "dwpw_valu_kernel<%d,%d,%d,%s>", K, S, CO, db ? "true" : "false");
     return nm;
 }
 
@@ -779,6 +919,7 @@ static bool img_form(const DwPwParams &p) {
         return e ? std::atoi(e) : 0;
     }();
     const int P = p.g.P;
+    if (mode == 5 && p.k != 5) return false;  // ZR_DWPW_IMG=5: 5x5 layers only
     // the tile's images must be one contiguous run per channel (CNHW activations)
     if (!mode || P > IBN || p.g.ncols % P != 0 || P % p.OW != 0 || p.in.sN != (int64_t)p.in.H * p.in.W)
         return false;

@@ -14,6 +14,7 @@
 // Reference: the 1x1 Conv / Gemm nodes of the four ONNX graphs executed by ORT/tract at
 // crates/zaru/src/nn/mod.rs:483-533.
 #include "../runtime/zr_kernels.h"
+#include <cstdlib>
 #include "act.h"
 #include "epilogue.h"
 
@@ -182,6 +183,76 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const GemmParams P, int
     }
 }
 
+// ---------------------------------------------------------------- image-row variant
+// Full-plane convolutions on a 1-position output (the landmark heads: 3x3 conv over a 3x3
+// plane, M = 1404 / 1, K = Cin * 9) with the images as the GEMM's rows: C^T[n][m] =
+// X^T[n][k] . W^T[k][m].  The column-per-image form reads X with a stride of one image per lane
+// and stores each output row with a stride of M per lane; here a lane's B fragment
+// W^T[k][m0 + lane % 32] and its stores out[n][m0 + lane % 32] are coalesced 128-B rows, and
+// the A fragment X^T[n0 + lane % 32][k] stays L1/L2-resident (the 4 waves of a workgroup share
+// it: 32 images x 4 M-tiles).  The next 32-deep K-chunk's fragments are loaded while the
+// current chunk's 16 MFMAs run.
+template <bool FULLPLANE>
+__global__ __launch_bounds__(256) void gemm_rows_kernel(const GemmParams P, int mtiles) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int kh = lane >> 5, col = lane & 31;
+    const int mt = blockIdx.y * 4 + wave;
+    if (mt >= mtiles) return;  // no barriers in this kernel
+    const int m0 = mt * 32, n0 = blockIdx.x * 32;
+    const int nimg = P.ncols;  // P == 1: one column per image
+    const int na = min(n0 + col, nimg - 1);
+    const float *xa = P.x + (int64_t)na * P.x_sN;
+    const float *wb = P.wt + m0 + col;  // [Kpad][Mpad]
+
+    float a[2][KC / 2], b[2][KC / 2];
+    auto load = [&](int kc, int buf) {
+#pragma unroll
+        for (int s = 0; s < KC / 2; ++s) {
+            const int k = kc + 2 * s + kh;
+            const int kcl = k < P.K ? k : P.K - 1;
+            float v;
+            if constexpr (FULLPLANE) {
+                const int ci = kcl / P.KK, kq = kcl - ci * P.KK;
+                v = xa[(int64_t)ci * P.x_sC + (int64_t)kq * P.x_sK];
+            } else {
+                v = xa[(int64_t)kcl * P.x_sC];
+            }
+            a[buf][s] = k < P.K ? v : 0.f;
+            b[buf][s] = wb[(int64_t)(k < P.Kpad ? k : 0) * P.Mpad];
+            if (k >= P.Kpad) b[buf][s] = 0.f;
+        }
+    };
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    load(0, 0);
+    for (int kc = 0; kc < P.Kpad; kc += 2 * KC) {
+        if (kc + KC < P.Kpad) load(kc + KC, 1);
+#pragma unroll
+        for (int s = 0; s < KC / 2; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][s], b[0][s], acc, 0, 0, 0);
+        if (kc + KC >= P.Kpad) break;
+        if (kc + 2 * KC < P.Kpad) load(kc + 2 * KC, 0);
+#pragma unroll
+        for (int s = 0; s < KC / 2; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][s], b[1][s], acc, 0, 0, 0);
+    }
+
+    // acc[r] = C^T[n0 + mfma32_row(r, kh)][m0 + col]
+    const int m = m0 + col;
+    if (m >= P.M) return;
+    const float bias = P.bias[m];
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = acc[r] + bias;
+    auto chan = [&](int) { return m; };
+    apply_act_n<16>(P.pre, v, chan);
+    apply_act_n<16>(P.post, v, chan);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int n = n0 + mfma32_row(r, kh);
+        if (n < nimg) P.out[(uint32_t)n * (uint32_t)P.o_sN + (uint32_t)m * (uint32_t)P.o_sC] = v[r];
+    }
+}
+
 template <int MT, int NT>
 static const char *launch_tiled(const GemmParams &p, hipStream_t s) {
     constexpr int BN = 4 * NT * 32;
@@ -217,6 +288,14 @@ static const char *launch_mt(const GemmParams &p, dim3 grid, hipStream_t s) {
     return names[p.KK > 1][MT];
 }
 
+static bool rows_form() {  // ZR_GEMM_ROWS=0 disables the image-row form (A/B runs)
+    static const int mode = [] {
+        const char *e = std::getenv("ZR_GEMM_ROWS");
+        return e ? std::atoi(e) : 1;
+    }();
+    return mode != 0;
+}
+
 const char *launch_gemm(const GemmParams &p, hipStream_t s) {
     const int mtiles = p.Mpad / 32;
     // LDS-tiled path: X must be a row-major [K][ncols] matrix with 16-B aligned rows
@@ -232,6 +311,11 @@ const char *launch_gemm(const GemmParams &p, hipStream_t s) {
         // keep >= ~2 workgroups per CU: trade M-tile reuse for parallelism on small problems
         while (mt > 1 && (int64_t)((p.ncols + bn - 1) / bn) * ((mtiles + mt - 1) / mt) < 512) --mt;
         return nt == 2 ? launch_tiled_nt<2>(p, mt, s) : launch_tiled_nt<1>(p, mt, s);
+    }
+    if (p.P == 1 && p.res_mode == 0 && p.KK > 1 && rows_form()) {  // a head over whole planes
+        dim3 grid((p.ncols + 31) / 32, (mtiles + 3) / 4);
+        hipLaunchKernelGGL((gemm_rows_kernel<true>), grid, dim3(256), 0, s, p, mtiles);
+        return "gemm_rows_kernel<true>";
     }
     const int bx = (p.ncols + 127) / 128;
     // Largest M tile (operand reuse) that still leaves >= 2 workgroups per CU of parallelism.
