@@ -205,17 +205,23 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(const GemmParams P, int 
     const float *wb = P.wt + m0 + col;  // [Kpad][Mpad]
 
     float a[2][KC / 2], b[2][KC / 2];
+    // k = ci * KK + kq of this lane's next A element, advanced by 2 per k-step (KK >= 2: at most
+    // one wrap), so no per-element integer division
+    int ci = 0, kq = kh;
     auto load = [&](int kc, int buf) {
 #pragma unroll
         for (int s = 0; s < KC / 2; ++s) {
             const int k = kc + 2 * s + kh;
-            const int kcl = k < P.K ? k : P.K - 1;
             float v;
             if constexpr (FULLPLANE) {
-                const int ci = kcl / P.KK, kq = kcl - ci * P.KK;
-                v = xa[(int64_t)ci * P.x_sC + (int64_t)kq * P.x_sK];
+                const bool in = k < P.K;
+                v = xa[in ? (uint32_t)ci * (uint32_t)P.x_sC + (uint32_t)kq * (uint32_t)P.x_sK : 0u];
+                kq += 2;
+                const bool wrap = kq >= P.KK;
+                kq -= wrap ? P.KK : 0;
+                ci += wrap ? 1 : 0;
             } else {
-                v = xa[(int64_t)kcl * P.x_sC];
+                v = xa[(int64_t)(k < P.K ? k : P.K - 1) * P.x_sC];
             }
             a[buf][s] = k < P.K ? v : 0.f;
             b[buf][s] = wb[(int64_t)(k < P.Kpad ? k : 0) * P.Mpad];
@@ -312,7 +318,7 @@ const char *launch_gemm(const GemmParams &p, hipStream_t s) {
         while (mt > 1 && (int64_t)((p.ncols + bn - 1) / bn) * ((mtiles + mt - 1) / mt) < 512) --mt;
         return nt == 2 ? launch_tiled_nt<2>(p, mt, s) : launch_tiled_nt<1>(p, mt, s);
     }
-    if (p.P == 1 && p.res_mode == 0 && p.KK > 1 && rows_form()) {  // a head over whole planes
+    if (p.P == 1 && p.res_mode == 0 && p.KK > 1 && rows_form()) {  // a head over whole planes (KK >= 2)
         dim3 grid((p.ncols + 31) / 32, (mtiles + 3) / 4);
         hipLaunchKernelGGL((gemm_rows_kernel<true>), grid, dim3(256), 0, s, p, mtiles);
         return "gemm_rows_kernel<true>";
