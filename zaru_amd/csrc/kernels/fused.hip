@@ -755,6 +755,150 @@ __global__ __launch_bounds__(256) void dwpw_img_kernel(const DwPwParams P, int G
     }
 }
 
+// LDS-DMA form of the MFMA dwpw for the stride-1 low-resolution layers (24^2 ... 6^2 planes
+// with 64-256 channels), whose register-staged form waits on memory most of the time.  Per
+// chunk of DFKC input channels one buffer receives, by global_load_lds_dwordx4 (no VGPRs, no
+// staging instructions beyond the address math), the contiguous CNHW run of input each channel
+// needs for the tile's BN columns (images are contiguous inside a channel: the run from the
+// first needed row of the first image to the last needed row of the last one), the chunk's
+// rows of the transposed 1x1 weights, and its depthwise weights and biases.  Two buffers: the
+// next chunk's copy is in flight while this chunk's depthwise (from LDS) and MFMAs run; the
+// barrier that publishes the depthwise tile to the MFMAs is a bare s_barrier, so it does not
+// drain that copy.
+constexpr int DFKC = 16;
+
+template <int K, int S, int WM, int MTW>
+__global__ __launch_bounds__(256) void dwpw_dma_kernel(const DwPwParams P, int nct, int runmax, int bufsz) {
+    constexpr int WN = 4 / WM, BN = WN * 32, BM = WM * MTW * 32, KK = K * K;
+    constexpr int CPAR = 256 / BN, PER = DFKC / CPAR;
+    constexpr int KKP = (DFKC * KK + 3) / 4 * 4;
+    // [guard: 256 words] [2 x bufsz] [sD: DFKC x BN]; masked taps of the first run may index up
+    // to pad_t * W + pad_l words before it, into the guard rather than out of the allocation
+    extern __shared__ __attribute__((aligned(16))) float lds_all[];
+    float *smem = lds_all + 256;
+    float *sD = smem + 2 * bufsz;
+    const GemmParams &G = P.g;
+
+    const int cpx = gridDim.x >> 3;  // gridDim.x is a multiple of 8
+    const int tile = (blockIdx.x & 7) * cpx + (blockIdx.x >> 3);
+    if (tile >= nct) return;  // whole workgroup, before any barrier
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kh = lane >> 5, col = lane & 31;
+    const int wm = wave % WM, wn = wave / WM;
+    const int j0 = tile * BN, m0 = blockIdx.y * BM;
+    const int Cin = G.K, H = P.in.H, W = P.in.W, Pin = H * W, OW = P.OW, Pq = G.P;
+    const int pt = P.pad_t, pl = P.pad_l;
+
+    // the input run of this tile (floats from a channel's base; 16-byte aligned ends)
+    const int ja = j0, jb = min(j0 + BN, G.ncols) - 1;
+    const int na = ja / Pq, qa = ja - na * Pq, nb = jb / Pq, qb = jb - nb * Pq;
+    const int ya = max(qa / OW * S - pt, 0), yb = min(qb / OW * S - pt + K - 1, H - 1);
+    const int s0 = (na * Pin + ya * W) & ~3;
+    const int e0 = (nb * Pin + (yb + 1) * W + 3) & ~3;
+    const int run4 = (e0 - s0) >> 2;  // <= runmax / 4
+
+    // slot regions of a buffer (16-byte slots)
+    const int rq = runmax >> 2;
+    const int r1 = DFKC * rq, r2 = r1 + DFKC * (BM / 4), r3 = r2 + KKP / 4, r4 = r3 + DFKC / 4;
+    const float inv_rq = 1.f / (float)rq;
+    const int nwi = bufsz >> 8;  // 64-slot DMA wave-instructions per buffer
+    auto stage = [&](int kc, float *dst) {
+        for (int wi = wave; wi < nwi; wi += 4) {
+            const int sl = wi * 64 + lane;
+            const float *src = (const float *)&zr_zero4;
+            if (sl < r1) {
+                const int c = qdiv(sl, rq, inv_rq), i = sl - c * rq;
+                if (kc + c < Cin && i < run4)
+                    src = P.in.p + (size_t)(uint32_t)(kc + c) * (uint32_t)P.in.sC + (uint32_t)(s0 + 4 * i);
+            } else if (sl < r2) {
+                const int r = (sl - r1) / (BM / 4), i = sl - r1 - r * (BM / 4);
+                if (kc + r < G.Kpad && m0 + 4 * i < G.Mpad)
+                    src = G.wt + (size_t)(uint32_t)(kc + r) * (uint32_t)G.Mpad + (uint32_t)(m0 + 4 * i);
+            } else if (sl < r3) {
+                const int i = sl - r2;
+                if (kc * KK + 4 * i < Cin * KK) src = P.dw_w + kc * KK + 4 * i;
+            } else if (sl < r4) {
+                const int i = sl - r3;
+                if (kc + 4 * i < Cin) src = P.dw_b + kc + 4 * i;
+            }
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                             (__attribute__((address_space(3))) void *)(dst + wi * 256), 16, 0, 0);
+        }
+    };
+
+    // depthwise role: column dj, channels dc, dc + CPAR, ... of each chunk
+    const int dj = tid % BN;
+    int dc = tid / BN;
+    if constexpr (BN >= 64) dc = __builtin_amdgcn_readfirstlane(dc);  // one channel per wave
+    const int jd = min(j0 + dj, G.ncols - 1);
+    const int n = jd / Pq, q = jd - n * Pq;
+    const int oy = q / OW, ox = q - oy * OW;
+    const int iy0 = oy * S - pt, ix0 = ox * S - pl;
+    const int tb = n * Pin + iy0 * W + ix0 - s0;  // run index of tap (0, 0) (may be < 0 when masked)
+    uint32_t mask = 0;
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) {
+            const int iy = iy0 + ky, ix = ix0 + kx;
+            mask |= (iy >= 0 && iy < H && ix >= 0 && ix < W ? 1u : 0u) << (ky * K + kx);
+        }
+
+    f32x16 acc[MTW];
+#pragma unroll
+    for (int t = 0; t < MTW; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+    stage(0, smem);
+    for (int kc = 0, it = 0; kc < Cin; kc += DFKC, ++it) {
+        const float *buf = smem + (it & 1) * bufsz;
+        __syncthreads();  // vmcnt(0) + barrier: this chunk has landed; last chunk's readers are done
+        if (kc + DFKC < Cin) stage(kc + DFKC, smem + ((it + 1) & 1) * bufsz);
+        const float *sIn = buf, *sW = buf + DFKC * runmax, *sDW = sW + DFKC * BM, *sDB = sDW + KKP;
+        float dv[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int c = dc + CPAR * i;
+            const float *t0 = sIn + c * runmax + tb;
+            const float *w = sDW + c * KK;
+            float a = sDB[c];
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx) {
+                    const int t = ky * K + kx;
+                    const float x = t0[ky * W + kx];
+                    a = __builtin_fmaf(w[t], ((mask >> t) & 1u) ? x : 0.f, a);
+                }
+            dv[i] = a;
+        }
+        apply_act_n<PER>(P.dw_act, dv, [&](int i) {
+            const int c = kc + dc + CPAR * i;
+            return c < Cin ? c : Cin - 1;
+        });
+#pragma unroll
+        for (int i = 0; i < PER; ++i) sD[(dc + CPAR * i) * BN + dj] = kc + dc + CPAR * i < Cin ? dv[i] : 0.f;
+        // publish sD without draining the next chunk's DMA (a __syncthreads would wait vmcnt(0))
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+        for (int s = 0; s < DFKC / 2; ++s) {
+            float a[MTW];
+#pragma unroll
+            for (int t = 0; t < MTW; ++t) a[t] = sW[(2 * s + kh) * BM + (wm * MTW + t) * 32 + col];
+            const float b = sD[(2 * s + kh) * BN + wn * 32 + col];
+#pragma unroll
+            for (int t = 0; t < MTW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t], b, acc[t], 0, 0, 0);
+        }
+    }
+
+    const int j = j0 + wn * 32 + col;
+    if (j >= G.ncols) return;
+    const int on = j / Pq, oq = j - on * Pq;
+#pragma unroll
+    for (int t = 0; t < MTW; ++t) epilogue_tile(G, acc[t], on, oq, m0 + (wm * MTW + t) * 32, kh);
+}
+
 bool dwpw_supported(int k, int stride) { return (k == 3 || k == 5) && (stride == 1 || stride == 2); }
 
 namespace {
@@ -781,12 +925,53 @@ static bool v4_ok(const DwPwParams &p) {
            p.g.ncols % 4 == 0 && p.g.P % 4 == 0;
 }
 
+// LDS bytes of the DMA form for this layer and tile (0 when it does not apply): the longest
+// input run any BN-column tile needs, rounded to 16 B, and whole 1 KiB DMA wave-instructions.
+template <int K, int S, int WM, int MTW>
+static size_t dma_plan(const DwPwParams &p, int *runmax, int *bufsz) {
+    static const int mode = [] {  // ZR_DWPW_DMA=0 disables the form, 1 limits it to stride 1
+        const char *e = std::getenv("ZR_DWPW_DMA");
+        return e ? std::atoi(e) : 2;
+    }();
+    constexpr int BN = (4 / WM) * 32, BM = WM * MTW * 32, KKP = (DFKC * K * K + 3) / 4 * 4;
+    const int H = p.in.H, W = p.in.W, Pin = H * W, Pq = p.g.P, OW = p.OW;
+    const int nimg = p.g.ncols / Pq;
+    if (!mode || (S == 2 && mode < 2) || p.in.sN != Pin || p.in.sC % 4 || ((int64_t)nimg * Pin) % 4 || p.g.K % 4 ||
+        ((uintptr_t)p.in.p | (uintptr_t)p.g.wt | (uintptr_t)p.dw_w | (uintptr_t)p.dw_b) % 16)
+        return 0;
+    int rm = 0;
+    for (int j0 = 0; j0 < p.g.ncols; j0 += BN) {  // tiles repeat with the image period
+        const int jb = std::min(j0 + BN, p.g.ncols) - 1;
+        const int na = j0 / Pq, qa = j0 - na * Pq, nb = jb / Pq, qb = jb - nb * Pq;
+        const int ya = std::max(qa / OW * S - p.pad_t, 0), yb = std::min(qb / OW * S - p.pad_t + K - 1, H - 1);
+        const int s0 = (na * Pin + ya * W) & ~3, e0 = (nb * Pin + (yb + 1) * W + 3) & ~3;
+        rm = std::max(rm, e0 - s0);
+        if (na >= 4 && (j0 % Pq) == 0) break;  // the pattern has repeated (whole images seen)
+    }
+    const int words = DFKC * rm + DFKC * BM + KKP + DFKC;
+    *runmax = rm;
+    *bufsz = (words + 255) / 256 * 256;
+    if (p.pad_t * W + p.pad_l > 256) return 0;  // the guard in front of the buffers
+    const size_t lds = sizeof(float) * (256 + 2 * (size_t)*bufsz + DFKC * BN);
+    return lds <= 80 * 1024 ? lds : 0;
+}
+
 template <int K, int S, int WM, int MTW>
 const char *dwpw_go(const DwPwParams &p, hipStream_t s) {
     constexpr int BN = (4 / WM) * 32, BM = WM * MTW * 32;
     const int nct = (p.g.ncols + BN - 1) / BN;
     const int mb = (p.g.Mpad + BM - 1) / BM;
     dim3 grid((nct + 7) / 8 * 8, mb);
+    {
+        int runmax = 0, bufsz = 0;
+        if (const size_t lds = dma_plan<K, S, WM, MTW>(p, &runmax, &bufsz)) {
+            hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
+            static char dn[2][2][5][5][48];
+            char *nm = dn[K == 5][S == 2][WM][MTW];
+            if (!nm[0]) snprintf(nm, 48, "dwpw_dma_kernel<%d,%d,%d,%d>", K, S, WM, MTW);
+            return nm;
+        }
+    }
     const bool v4 = v4_ok(p);
     if (v4) hipLaunchKernelGGL((dwpw_kernel<K, S, WM, MTW, 1, true>), grid, dim3(256), 0, s, p, nct);
     else hipLaunchKernelGGL((dwpw_kernel<K, S, WM, MTW, 1, false>), grid, dim3(256), 0, s, p, nct);
