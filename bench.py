@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--sub-batches", type=int, default=2)
+    ap.add_argument("--sub-batches", type=int, default=3)
     ap.add_argument("--streams", choices=["multi", "single"], default="multi")
     ap.add_argument("--no-cross-step", action="store_true",
                     help="one pipeline call per step (no overlap across step boundaries)")

@@ -503,9 +503,9 @@ __device__ const float4 zr_zero4 = {0.f, 0.f, 0.f, 0.f};  // LDS-DMA source of t
 // next chunk's copy in flight while the current chunk is computed (one barrier per chunk).  The
 // staged image is slot-linear (slot = 16 B; row stride lw = 4 * srow floats), exactly the
 // lane-linear order one DMA wave-instruction writes; zero slots (padding) read zr_zero4.
-template <int K, int S, int CO, bool DB>
+template <int K, int S, int CO, bool DB, int VF>
 __global__ __launch_bounds__(256) void dwpw_valu_kernel(const DwPwParams P, int tpi, int ntiles, int bufsz, int lw) {
-    extern __shared__ __attribute__((aligned(16))) float sIn[];  // [VFKC * rows][lw]
+    extern __shared__ __attribute__((aligned(16))) float sIn[];  // [VF * rows][lw]
     const GemmParams &G = P.g;
     const int cpx = gridDim.x >> 3;  // gridDim.x is a multiple of 8
     const int tile = (blockIdx.x & 7) * cpx + (blockIdx.x >> 3);
@@ -515,7 +515,7 @@ __global__ __launch_bounds__(256) void dwpw_valu_kernel(const DwPwParams P, int 
     const int Pq = G.P, H = P.in.H, W = P.in.W, Cin = G.K, OW = P.OW;
     const int oy_a = q0 / OW, oy_b = min(q0 + VTQ - 1, Pq - 1) / OW;
     const int iy_a = oy_a * S - P.pad_t;
-    const int R = (oy_b - oy_a) * S + K;  // VFKC * R * lw <= bufsz (floats per LDS buffer)
+    const int R = (oy_b - oy_a) * S + K;  // VF * R * lw <= bufsz (floats per LDS buffer)
     const int q = min(q0 + tid, Pq - 1);
     const int oy = q / OW, ox = q - oy * OW;
     // LDS row layout: 4 zero floats, the W input values, >= 4 zero floats (lw % 4 == 0)
@@ -528,10 +528,43 @@ __global__ __launch_bounds__(256) void dwpw_valu_kernel(const DwPwParams P, int 
 #pragma unroll
     for (int i = 0; i < CO / 2; ++i) acc[i] = (f32x2)(0.f);
 
-    const int total = VFKC * R * srow;
+    const int total = VF * R * srow;
+    // The slot -> (channel, row, column) decomposition is the same for every chunk: for the
+    // (at most 4 * DMAX) DMA wave-instructions of a buffer it is computed once, as the slot's
+    // offset from the chunk's first channel plane (-1: a zero slot) and its channel.
+    constexpr int DMAX = DB ? 6 : 1;
+    const int nwi = (total + 63) >> 6, lane = tid & 63, wave = tid >> 6;
+    const bool pre_off = nwi <= 4 * DMAX;
+    int goff[DMAX], gch[DMAX];
+    if constexpr (DB) {
+#pragma unroll
+        for (int m = 0; m < DMAX; ++m) {
+            const int sl = (wave + 4 * m) * 64 + lane;
+            const int cr = qdiv(sl, srow, inv_srow), sx = sl - cr * srow;
+            const int c = qdiv(cr, R, inv_R), r = cr - c * R;
+            const int iy = iy_a + r, xv = sx - 1;
+            const bool ok = sl < total && iy >= 0 && iy < H && xv >= 0 && 4 * xv < W;
+            goff[m] = ok ? (int)((uint32_t)c * (uint32_t)P.in.sC + nbase + (uint32_t)(iy * W + 4 * xv)) : -1;
+            gch[m] = c;
+        }
+    }
     auto stage_dma = [&](int kc, float *dst) {
-        const int nwi = (total + 63) >> 6, lane = tid & 63;
-        for (int wi = tid >> 6; wi < nwi; wi += 4) {
+        if (pre_off) {
+            const float *base = P.in.p + (size_t)(uint32_t)kc * (uint32_t)P.in.sC;
+            const int cl = Cin - kc;
+#pragma unroll
+            for (int m = 0; m < DMAX; ++m) {
+                const int wi = wave + 4 * m;
+                if (wi < nwi) {
+                    const bool ok = goff[m] >= 0 && gch[m] < cl;
+                    const float *src = ok ? base + (uint32_t)goff[m] : (const float *)&zr_zero4;
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                                     (__attribute__((address_space(3))) void *)(dst + wi * 256), 16, 0, 0);
+                }
+            }
+            return;
+        }
+        for (int wi = wave; wi < nwi; wi += 4) {
             const int sl = wi * 64 + lane;
             const int cr = qdiv(sl, srow, inv_srow), sx = sl - cr * srow;
             const int c = qdiv(cr, R, inv_R), r = cr - c * R;
@@ -545,12 +578,12 @@ __global__ __launch_bounds__(256) void dwpw_valu_kernel(const DwPwParams P, int 
     };
     if constexpr (DB) stage_dma(0, sIn);
 
-    for (int kc = 0, it = 0; kc < Cin; kc += VFKC, ++it) {
+    for (int kc = 0, it = 0; kc < Cin; kc += VF, ++it) {
         const float *buf = sIn;
         if constexpr (DB) {
             buf = sIn + (it & 1) * bufsz;
-            __syncthreads();  // vmcnt(0) + barrier: chunk kc has landed, chunk kc - VFKC's readers are done
-            if (kc + VFKC < Cin) stage_dma(kc + VFKC, sIn + ((it + 1) & 1) * bufsz);
+            __syncthreads();  // vmcnt(0) + barrier: chunk kc has landed, chunk kc - VF's readers are done
+            if (kc + VF < Cin) stage_dma(kc + VF, sIn + ((it + 1) & 1) * bufsz);
         } else
         for (int base = 0; base < total; base += 1024) {
             float4 v[4];
@@ -576,7 +609,7 @@ __global__ __launch_bounds__(256) void dwpw_valu_kernel(const DwPwParams P, int 
         }
         if constexpr (!DB) __syncthreads();
 #pragma unroll 2
-        for (int c = 0; c < VFKC; ++c) {
+        for (int c = 0; c < VF; ++c) {
             const int ch = kc + c;
             if (ch >= Cin) break;
             const float *t0 = buf + c * R * lw + lb;
@@ -1037,27 +1070,37 @@ const char *dwpw_valu_go(const DwPwParams &p, hipStream_t s) {
         rmax = std::max(rmax, (b - a) * S + K);
     }
     const int lw = p.in.W + 8;
-    // double-buffered LDS-DMA staging for the 32-channel outputs, whose 131 VGPRs hold a CU to
-    // 3 workgroups anyway (two buffers of <= 32 KiB keep that); at 16 channels 5 workgroups fit
-    // by registers and the second buffer would cost occupancy, at 48 it measured slower.
-    // ZR_VALU_DB=0 disables it (A/B runs), 2 allows it for every CO.
+    // Double-buffered LDS-DMA staging (ZR_VALU_DB=0 disables it for A/B runs).  Measured per CO:
+    // 32 channels: 8-channel chunks while two buffers fit 64 KiB (the 131 VGPRs hold a CU to 3
+    // workgroups anyway), else 4-channel chunks; 16 channels: 4-channel chunks, so two buffers
+    // cost no more LDS (and occupancy) than one 8-channel buffer; 48 channels: only at stride 2
+    // (slower at stride 1).
     static const int db_mode = [] {
         const char *e = std::getenv("ZR_VALU_DB");
         return e ? std::atoi(e) : 1;
     }();
-    const int bufsz = (VFKC * rmax * lw + 255) / 256 * 256;  // whole 1 KiB DMA wave-instructions
-    const bool db = db_mode && (CO == 32 || db_mode == 2) && 2 * sizeof(float) * (size_t)bufsz <= 64 * 1024;
+    auto buf_of = [&](int vf) { return (vf * rmax * lw + 255) / 256 * 256; };  // whole 1 KiB DMA rows
+    const bool fit8 = 2 * sizeof(float) * (size_t)buf_of(VFKC) <= 64 * 1024;
+    const bool db = db_mode && (CO == 16 || CO == 32 || (CO == 48 && S == 2)) &&
+                    2 * sizeof(float) * (size_t)buf_of(4) <= 64 * 1024;
+    const bool small = db && !(CO == 32 && fit8);
+    const int vf = small ? 4 : VFKC;
+    const int bufsz = buf_of(vf);
     dim3 grid((ntiles + 7) / 8 * 8);
     if (db) {
         const size_t lds = 2 * sizeof(float) * (size_t)bufsz;
-        hipLaunchKernelGGL((dwpw_valu_kernel<K, S, CO, true>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
+        if (small)
+            hipLaunchKernelGGL((dwpw_valu_kernel<K, S, CO, true, 4>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
+        else
+            hipLaunchKernelGGL((dwpw_valu_kernel<K, S, CO, true, VFKC>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
     } else {
         const size_t lds = sizeof(float) * (size_t)VFKC * rmax * lw;
-        hipLaunchKernelGGL((dwpw_valu_kernel<K, S, CO, false>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
+        hipLaunchKernelGGL((dwpw_valu_kernel<K, S, CO, false, VFKC>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
     }
-    static char names[2][2][5][2][56];
-    char *nm = names[K == 5][S == 2][CO / 16][db];
-    if (!nm[0]) snprintf(nm, 56, "dwpw_valu_kernel<%d,%d,%d,%s>", K, S, CO, db ? "true" : "false");
+    static char names[2][2][5][2][2][56];
+    const int vfe = db ? vf : VFKC;
+    char *nm = names[K == 5][S == 2][CO / 16][db][vfe == 4];
+    if (!nm[0]) snprintf(nm, 56, "dwpw_valu_kernel<%d,%d,%d,%s,%d>", K, S, CO, db ? "true" : "false", vfe);
     return nm;
 }
 
