@@ -38,8 +38,8 @@ FP32_PEAK_TFLOPS = 157.3   # f32 MFMA = f32 VALU peak
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1024, help="frames per step per GPU")
     ap.add_argument("--workload", choices=["face", "hand"], default="face")
     ap.add_argument("--threads", type=int, default=16, help="host decode/map threads per rank")

@@ -1074,14 +1074,14 @@ const char *dwpw_valu_go(const DwPwParams &p, hipStream_t s) {
     // 32 channels: 8-channel chunks while two buffers fit 64 KiB (the 131 VGPRs hold a CU to 3
     // workgroups anyway), else 4-channel chunks; 16 channels: 4-channel chunks, so two buffers
     // cost no more LDS (and occupancy) than one 8-channel buffer; 48 channels: only at stride 2
-    // (slower at stride 1).
+    // (slower at stride 1; ZR_VALU_DB=2 takes it there too).
     static const int db_mode = [] {
         const char *e = std::getenv("ZR_VALU_DB");
         return e ? std::atoi(e) : 1;
     }();
     auto buf_of = [&](int vf) { return (vf * rmax * lw + 255) / 256 * 256; };  // whole 1 KiB DMA rows
     const bool fit8 = 2 * sizeof(float) * (size_t)buf_of(VFKC) <= 64 * 1024;
-    const bool db = db_mode && (CO == 16 || CO == 32 || (CO == 48 && S == 2)) &&
+    const bool db = db_mode && (CO == 16 || CO == 32 || (CO == 48 && (S == 2 || db_mode == 2))) &&
                     2 * sizeof(float) * (size_t)buf_of(4) <= 64 * 1024;
     const bool small = db && !(CO == 32 && fit8);
     const int vf = small ? 4 : VFKC;
