@@ -37,6 +37,7 @@ SWITCHES = {
     "no_dma": {"ZR_DWPW_DMA": "0"},
     "no_v4": {"ZR_DWPW_V4": "0", "ZR_DWPW_DMA": "0"},
     "no_rows": {"ZR_GEMM_ROWS": "0"},
+    "dma_chunk32": {"ZR_DWPW_FKC": "32"},  # not an off-switch: the other DMA chunk size
 }
 
 
@@ -47,7 +48,7 @@ def outputs(tmp_path_factory):
     for name, env in SWITCHES.items():
         path = str(d / f"{name}.npz")
         e = dict(os.environ)
-        for k in ("ZR_VALU_DB", "ZR_DWPW_DMA", "ZR_DWPW_V4", "ZR_GEMM_ROWS"):
+        for k in ("ZR_VALU_DB", "ZR_DWPW_DMA", "ZR_DWPW_V4", "ZR_GEMM_ROWS", "ZR_DWPW_FKC"):
             e.pop(k, None)
         e.update(env)
         subprocess.run([sys.executable, "-c", CHILD, REPO, path], env=e, check=True, timeout=110)

@@ -798,9 +798,7 @@ __global__ __launch_bounds__(256) void dwpw_img_kernel(const DwPwParams P, int G
 // next chunk's copy is in flight while this chunk's depthwise (from LDS) and MFMAs run; the
 // barrier that publishes the depthwise tile to the MFMAs is a bare s_barrier, so it does not
 // drain that copy.
-constexpr int DFKC = 16;
-
-template <int K, int S, int WM, int MTW>
+template <int K, int S, int WM, int MTW, int DFKC>
 __global__ __launch_bounds__(256) void dwpw_dma_kernel(const DwPwParams P, int nct, int runmax, int bufsz) {
     constexpr int WN = 4 / WM, BN = WN * 32, BM = WM * MTW * 32, KK = K * K;
     constexpr int CPAR = 256 / BN, PER = DFKC / CPAR;
@@ -960,7 +958,7 @@ static bool v4_ok(const DwPwParams &p) {
 
 // LDS bytes of the DMA form for this layer and tile (0 when it does not apply): the longest
 // input run any BN-column tile needs, rounded to 16 B, and whole 1 KiB DMA wave-instructions.
-template <int K, int S, int WM, int MTW>
+template <int K, int S, int WM, int MTW, int DFKC>
 static size_t dma_plan(const DwPwParams &p, int *runmax, int *bufsz) {
     static const int mode = [] {  // ZR_DWPW_DMA=0 disables the form, 1 limits it to stride 1
         const char *e = std::getenv("ZR_DWPW_DMA");
@@ -996,12 +994,25 @@ const char *dwpw_go(const DwPwParams &p, hipStream_t s) {
     const int mb = (p.g.Mpad + BM - 1) / BM;
     dim3 grid((nct + 7) / 8 * 8, mb);
     {
+        // input channels per DMA chunk (ZR_DWPW_FKC=32: half the chunk barriers, twice the LDS)
+        static const int fkc = [] {
+            const char *e = std::getenv("ZR_DWPW_FKC");
+            return e && std::atoi(e) == 32 ? 32 : 16;
+        }();
         int runmax = 0, bufsz = 0;
-        if (const size_t lds = dma_plan<K, S, WM, MTW>(p, &runmax, &bufsz)) {
-            hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
+        if (fkc == 32) {
+            if (const size_t lds = dma_plan<K, S, WM, MTW, 32>(p, &runmax, &bufsz)) {
+                hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, 32>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
+                static char dn[2][2][5][5][48];
+                char *nm = dn[K == 5][S == 2][WM][MTW];
+                if (!nm[0]) snprintf(nm, 48, "dwpw_dma_kernel<%d,%d,%d,%d,32>", K, S, WM, MTW);
+                return nm;
+            }
+        } else if (const size_t lds = dma_plan<K, S, WM, MTW, 16>(p, &runmax, &bufsz)) {
+            hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, 16>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
             static char dn[2][2][5][5][48];
             char *nm = dn[K == 5][S == 2][WM][MTW];
-            if (!nm[0]) snprintf(nm, 48, "dwpw_dma_kernel<%d,%d,%d,%d>", K, S, WM, MTW);
+            if (!nm[0]) snprintf(nm, 48, "dwpw_dma_kernel<%d,%d,%d,%d,16>", K, S, WM, MTW);
             return nm;
         }
     }
@@ -1194,6 +1205,10 @@ const char *launch_dwpw(const DwPwParams &p, hipStream_t s) {
         if (p.k == 3) return p.stride == 1 ? dwpw_rows_mt<3, 1>(p, s) : dwpw_rows_mt<3, 2>(p, s);
         return p.stride == 1 ? dwpw_rows_mt<5, 1>(p, s) : dwpw_rows_mt<5, 2>(p, s);
     }
+    static const int64_t min_wgs = [] {  // workgroups one launch should reach (ZR_DWPW_MINWG)
+        const char *e = std::getenv("ZR_DWPW_MINWG");
+        return e ? (int64_t)std::atoll(e) : (int64_t)1024;
+    }();
     const DwPwLayout *best = nullptr;
     int64_t best_wgs = 0;
     for (const DwPwLayout &l : kLayouts) {
@@ -1203,8 +1218,8 @@ const char *launch_dwpw(const DwPwParams &p, hipStream_t s) {
         const int64_t wgs = (int64_t)((p.g.ncols + l.bn() - 1) / l.bn()) * mb;
         bool better;
         if (!best) better = true;
-        else if ((wgs >= 1024) != (best_wgs >= 1024)) better = wgs >= 1024;
-        else if (wgs >= 1024) better = l.bn() > best->bn() || (l.bn() == best->bn() && l.bm() < best->bm());
+        else if ((wgs >= min_wgs) != (best_wgs >= min_wgs)) better = wgs >= min_wgs;
+        else if (wgs >= min_wgs) better = l.bn() > best->bn() || (l.bn() == best->bn() && l.bm() < best->bm());
         else better = wgs > best_wgs || (wgs == best_wgs && l.bm() < best->bm());
         if (better) {
             best = &l;
