@@ -125,6 +125,8 @@ def _lib():
     L.zo_tracker_update.restype = C.c_int
     L.zo_tracker_update.argtypes = [P, sz, C.POINTER(RRect), f, f, f, C.POINTER(RRect),
                                     C.POINTER(RRect)]
+    L.zo_landmark_angle.restype = f
+    L.zo_landmark_angle.argtypes = [C.c_int, P]
     L.zo_net_load.restype = P
     L.zo_net_load.argtypes = [P, sz, C.c_int]
     L.zo_net_num_outputs.restype = sz
@@ -273,6 +275,24 @@ def tracker_update(pos, view_rect: RRect, roi_rad, est_angle, padding):
     _lib().zo_tracker_update(_ptr(p), p.shape[0], C.byref(view_rect), roi_rad, est_angle,
                              padding, C.byref(upd), C.byref(nxt))
     return p, upd, nxt
+
+
+FACEMESH, HAND = 0, 1
+
+
+def landmark_angle(kind, pos) -> float:
+    """Estimate::angle_radians of view-local landmarks (FACEMESH: mediapipe.rs:146-160,
+    HAND: hand/landmark.rs:68-78)."""
+    p = np.ascontiguousarray(pos, np.float32)
+    return _lib().zo_landmark_angle(kind, _ptr(p))
+
+
+def landmark_confidence(kind, outs) -> float:
+    """Confidence::confidence of the raw landmark-network outputs: FaceMesh face_flag =
+    sigmoid(out1) (mediapipe.rs:60), hand presence = out1 (sigmoid inside the graph,
+    hand/landmark.rs:309)."""
+    v = float(np.asarray(outs[1], np.float32).reshape(-1)[0])
+    return sigmoid(v) if kind == FACEMESH else v
 
 
 # ---------------------------------------------------------------- networks

@@ -440,3 +440,17 @@ int zo_tracker_update(float *pos, size_t n, const zo_rrect *view_rect, float roi
     next_roi->rect = zo_rect_grow_rel(updated->rect, padding);
     return 1;
 }
+
+/* Estimate::angle_radians of the two landmark networks, on view-local positions (n x 3):
+ * FaceMesh V1 rotation_radians (mediapipe.rs:146-160): (right_eye 263 - left_eye 33)
+ *   .signed_angle_to(X);
+ * hand landmark rotation_radians (hand/landmark.rs:68-78): (wrist 0 - middle MCP 9)
+ *   .signed_angle_to(Y). */
+float zo_landmark_angle(int kind, const float *pos) {
+    if (kind == 0) {
+        float dx = pos[3 * 263] - pos[3 * 33], dy = pos[3 * 263 + 1] - pos[3 * 33 + 1];
+        return zo_signed_angle_to(dx, dy, 1.0f, 0.0f);
+    }
+    float dx = pos[0] - pos[3 * 9], dy = pos[1] - pos[3 * 9 + 1];
+    return zo_signed_angle_to(dx, dy, 0.0f, 1.0f);
+}

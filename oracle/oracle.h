@@ -83,6 +83,9 @@ void zo_estimator_map(float *pos, size_t n, const zo_rect *view_local_rect, uint
 /* LandmarkTracker::track_impl steps 4-5 (landmark.rs:479-494) */
 int zo_tracker_update(float *pos, size_t n, const zo_rrect *view_rect, float roi_rad,
                       float est_angle, float padding, zo_rrect *updated, zo_rrect *next_roi);
+/* Estimate::angle_radians (kind 0 FaceMesh V1, mediapipe.rs:146-160; 1 hand,
+ * hand/landmark.rs:68-78) of view-local positions (n x 3) */
+float zo_landmark_angle(int kind, const float *pos);
 
 /* ---- ONNX interpreter (nnexec) ---- */
 typedef struct zo_net zo_net;

@@ -8,6 +8,22 @@ definitions of SURVEY.md §8a:
 (iii) landmarks agree within L2 <= 1e-3 in the network-input pixel space (192 px FaceMesh,
       224 px hand), i.e. frame-pixel error / (view side / input side).
 
+and, for LandmarkTracker::track_impl (landmark.rs:463-501), on every ROI:
+  * the estimate's confidence (FaceMesh face_flag = sigmoid(out1), mediapipe.rs:60; hand
+    presence, hand/landmark.rs:309) within 1e-4 of the oracle's;
+  * tracked == (oracle confidence >= loss threshold 0.5) outside the same boundary band, and a
+    lost ROI publishes no landmarks (the reference returns None, landmark.rs:468-477);
+  * for tracked ROIs: the estimate angle (mediapipe.rs:146-160 / hand/landmark.rs:68-78) fed
+    to the oracle's tracker update, then landmarks (frame px), updated ROI
+    (RotatedRect::bounding, rect.rs:287-325) and next ROI (grow_rel(padding), landmark.rs:
+    488-494) against the oracle's.
+
+The pipeline runs at the production batch (256 frames, 3 sub-batches on their own streams: the
+bench's batch-dependent kernel tilings); the oracle re-computes a seeded sample of them.
+The hand frames hold no hands, so almost every hand ROI is lost at the reference's 0.5 loss
+threshold; a second run with loss threshold 0 (LandmarkTracker::set_loss_threshold) sends the
+same ROIs through the tracked branch so the hand mapping is compared too.
+
 Detection -> NMS -> mapping is bit-exact when fed the same raw tensors (test_host_cpu.py); here
 the raw tensors come from two different f32 evaluation orders, so (ii)/(iii) are the bar.
 """
@@ -25,11 +41,19 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MODELS = os.path.join(REPO, "zaru_amd", "models")
 BAND = 1e-5
 W, H = 1920, 1080
+BATCH = 256
+LM_L2_TOL = 1e-3      # network-input px (SURVEY §8a iii)
+CONF_TOL = 1e-4       # face_flag / presence probability
+ANGLE_TOL = 2e-4      # rad: estimate angle from two landmarks >= 8 network px apart
+RECT_TOL = 2e-2       # network-input px: bounding rect of landmarks rotated by that angle
 
 CASES = {
-    # kind: detector, landmark net, det input, landmark input, colour lo, NMS kind, grow, padding
-    "face": ("face_detection_short_range", "face_landmark", 128, 192, -1.0, O.FACE, 0.0, 0.3),
-    "hand": ("palm_detection_lite", "hand_landmark_lite", 192, 224, 0.0, O.PALM, 1.5, 0.4),
+    # kind: detector, landmark net, det input, landmark input, colour lo, NMS kind,
+    #       landmark kind, padding, checked frames
+    "face": ("face_detection_short_range", "face_landmark", 128, 192, -1.0, O.FACE,
+             O.FACEMESH, 0.3, 8),
+    "hand": ("palm_detection_lite", "hand_landmark_lite", 192, 224, 0.0, O.PALM,
+             O.HAND, 0.4, 5),
 }
 
 
@@ -41,11 +65,16 @@ def face_patch():
 
 
 def frames_for(kind, n, seed):
+    """n 1080p frames over 8 seeded noise backgrounds, each face frame (every frame for face,
+    every other one for hand) with the face patch at a seeded position; per frame seeded
+    forced ROIs (1 upright for face, 4 rotated for hand)."""
     rng = np.random.default_rng(seed)
-    frames = rng.integers(0, 256, size=(n, H, W, 4), dtype=np.uint8)
+    base = rng.integers(0, 256, size=(8, H, W, 4), dtype=np.uint8)
+    frames = np.empty((n, H, W, 4), np.uint8)
     patch = face_patch()
     for i in range(n):
-        if kind == "face" or i % 2 == 0:  # hand frames: half noise-only (forced ROIs)
+        frames[i] = base[i % len(base)]
+        if kind == "face" or i % 2 == 0:
             y, x = int(rng.integers(0, H - 576)), int(rng.integers(0, W - 576))
             frames[i, y:y + 576, x:x + 576] = patch
     forced = []
@@ -67,52 +96,69 @@ def H_():
     return Hm
 
 
+def rrect_close(got, want, per_px):
+    """RotatedRect (host binding) vs oracle RRect: angle within ANGLE_TOL, centre/size within
+    RECT_TOL network px."""
+    g = got.rect().tuple()
+    w = want.rect.tuple()
+    d_ang = abs(got.rotation_radians() - want.rad)
+    d_px = max(abs(a - b) for a, b in zip(g, w)) / per_px
+    return d_ang, d_px
+
+
 @pytest.mark.parametrize("kind", ["face", "hand"])
 def test_pipeline_vs_oracle_1080p(H_, kind):
     from zaru_amd._lib import DeviceBuffer
-    from zaru_amd.nn import Cnn, ColorMapper, NeuralNetwork, model_bytes
 
-    det_m, lm_m, din, lin, lo, okind, grow, pad = CASES[kind]
-    n = 4
-    frames, forced = frames_for(kind, n, 101 if kind == "face" else 102)
-    bufs = [DeviceBuffer.from_array(f) for f in frames]
-    flist = [(b.ptr, W, H, W * 4) for b in bufs]
-    p = H_.DetectTrackPipeline(kind, 0, 4, 1 if kind == "face" else 4)
-    p.run(flist, forced)
+    det_m, lm_m, din, lin, lo, okind, lkind, pad, n_check = CASES[kind]
+    frames, forced = frames_for(kind, BATCH, 101 if kind == "face" else 102)
+    buf = DeviceBuffer.from_array(frames)
+    fb = H * W * 4
+    flist = [(buf.ptr + i * fb, W, H, W * 4) for i in range(BATCH)]
+    per_frame = 1 if kind == "face" else 4
+    runs = {}
+    for loss in (0.5, 0.0):
+        p = H_.DetectTrackPipeline(kind, 0, 8, per_frame, 3, True, loss)
+        p.run(flist, forced)
+        runs[loss] = p
+        if kind == "face":
+            break  # every face ROI tracks at 0.5 already
+    p = runs[0.5]
 
-    det_gpu = Cnn(NeuralNetwork.from_onnx(model_bytes(det_m)).load(), ColorMapper.linear(lo, 1.0))
     det_cpu = O.Net(os.path.join(MODELS, det_m + ".onnx"), f64=False)
     lm_cpu = O.Net(os.path.join(MODELS, lm_m + ".onnx"), f64=False)
+    check = sorted(set(np.random.default_rng(7).choice(BATCH - 1, n_check - 1, replace=False).tolist())
+                   | {BATCH - 1})
 
     boundary = 0
-    worst_lm = 0.0
-    for f in range(n):
+    for f in check:
         img = frames[f]
         r = O.grow_to_fit_aspect(O.Rect.from_top_left(0, 0, W, H), din, din)
         v = O.view_compose(O.view_full(W, H), r)
-        reg_g, cls_g = det_gpu.estimate_views(img, [(v.rect.cx, v.rect.cy, v.rect.w, v.rect.h, v.rad)])
         reg_c, cls_c = det_cpu.run(O.preproc(img, v, din, din, lo, 1.0)[None])
-        # (ii) anchor selection: identical outside the boundary band
-        cg = np.array([O.sigmoid(float(t)) for t in cls_g.reshape(-1)], np.float32)
         cc = np.array([O.sigmoid(float(t)) for t in cls_c.reshape(-1)], np.float32)
-        sel_g, sel_c = cg >= 0.5, cc >= 0.5
-        near = np.abs(cc - 0.5) < BAND
-        boundary += int(near.sum())
-        assert np.array_equal(sel_g[~near], sel_c[~near]), (kind, f, np.nonzero(sel_g != sel_c))
-        # detections after NMS (frame px): the pipeline's vs the oracle chain's
+        boundary += int((np.abs(cc - 0.5) < BAND).sum())
+        # (ii) detections after NMS (frame px): the pipeline's vs the oracle chain's
         want = O.detect_post(okind, reg_c[0], cls_c[0], W, H, din, din)
         got = p.detections()[f]
-        assert len(got) == len(want), (kind, f)
+        assert len(got) == len(want), (kind, f, len(got), len(want))
         scale = W / din  # letterbox px per network px
         for a, b in zip(got, want):
-            assert abs(a.confidence() - b.conf) <= 1e-4
+            assert abs(a.confidence() - b.conf) <= CONF_TOL
+            assert abs(a.angle() - b.angle) <= ANGLE_TOL
             assert np.allclose(a.bounding_rect().tuple(), b.rect.tuple(), atol=2e-3 * scale)
     print(f"{kind}: anchors within the {BAND:g} boundary band: {boundary}")
     assert boundary == 0
 
-    # (iii) landmarks of every tracked ROI, recomputed by the oracle from the same ROI
-    checked = 0
-    for i in range(p.num_rois()):
+    # LandmarkTracker::track_impl on every ROI of the checked frames, from the same seed ROI
+    stats = {"rois": 0, "tracked": 0, "lost": 0, "band": 0, "lm_l2": 0.0, "ang": 0.0, "rect": 0.0,
+             "conf": 0.0, "degenerate": 0}
+    checked = set(check)
+    idx = {loss: [i for i in range(q.num_rois()) if q.roi(i)["frame"] in checked]
+           for loss, q in runs.items()}
+    for loss, q in runs.items():
+        assert len(idx[loss]) == len(idx[0.5])
+    for j, i in enumerate(idx[0.5]):
         rr = p.roi(i)
         img = frames[rr["frame"]]
         roi = rr["roi"]
@@ -123,12 +169,41 @@ def test_pipeline_vs_oracle_1080p(H_, kind):
         lrect = O.grow_to_fit_aspect(O.Rect.from_top_left(0, 0, view.rect.w, view.rect.h), 1, 1)
         v2 = O.view_compose(view, lrect)
         outs = lm_cpu.run(O.preproc(img, v2, lin, lin, lo, 1.0)[None])
+        conf = O.landmark_confidence(lkind, outs)
         pos = O.estimator_map(outs[0].reshape(-1, 3), lrect, lin)
-        want, _, _ = O.tracker_update(pos, vr, rad, 0.0, pad)
+        est_angle = O.landmark_angle(lkind, pos)
+        want, upd, nxt = O.tracker_update(pos, vr, rad, est_angle, pad)
         per_px = lrect.w / lin  # frame px per network-input px
-        l2 = np.sqrt(((rr["landmarks"][:, :2] - want[:, :2]) ** 2).sum(-1)).max() / per_px
-        worst_lm = max(worst_lm, float(l2))
-        assert l2 <= 1e-3, (kind, i, l2)
-        checked += 1
-    print(f"{kind}: {checked} ROIs, worst landmark L2 = {worst_lm:.2e} network px")
-    assert checked >= n
+        # the estimate angle is well-conditioned only when its two landmarks are apart
+        a, b = (263, 33) if lkind == O.FACEMESH else (0, 9)
+        sep = float(np.hypot(*(pos[a, :2] - pos[b, :2]))) / per_px
+        stats["rois"] += 1
+        for loss, q in runs.items():
+            r2 = q.roi(idx[loss][j])
+            assert r2["frame"] == rr["frame"] and r2["roi"].rect() == roi.rect()
+            stats["conf"] = max(stats["conf"], abs(r2["confidence"] - conf))
+            assert abs(r2["confidence"] - conf) <= CONF_TOL, (kind, i, r2["confidence"], conf)
+            if abs(conf - loss) < BAND:
+                stats["band"] += 1
+                continue
+            assert r2["tracked"] == (conf >= loss), (kind, i, loss, conf)
+            if not r2["tracked"]:
+                stats["lost"] += 1
+                assert r2["landmarks"].shape[0] == 0  # None in the reference
+                continue
+            stats["tracked"] += 1
+            l2 = np.sqrt(((r2["landmarks"][:, :2] - want[:, :2]) ** 2).sum(-1)).max() / per_px
+            stats["lm_l2"] = max(stats["lm_l2"], float(l2))
+            assert l2 <= LM_L2_TOL, (kind, i, loss, l2)
+            if sep < 8.0:
+                stats["degenerate"] += 1
+                continue
+            for got_r, want_r in ((r2["updated_roi"], upd), (r2["next_roi"], nxt)):
+                d_ang, d_px = rrect_close(got_r, want_r, per_px)
+                stats["ang"] = max(stats["ang"], d_ang)
+                stats["rect"] = max(stats["rect"], d_px)
+                assert d_ang <= ANGLE_TOL and d_px <= RECT_TOL, (kind, i, loss, d_ang, d_px)
+    print(f"{kind}: {stats}")
+    assert stats["rois"] >= len(check)
+    assert stats["tracked"] >= len(check) // 2
+    assert stats["band"] == 0

@@ -276,17 +276,19 @@ PYBIND11_MODULE(_zaru_host, m) {
 
     py::class_<DetectTrackPipeline>(m, "DetectTrackPipeline")
         .def(py::init([](const std::string &kind, int device, int threads, uint32_t max_rois,
-                         uint32_t sub_batches, bool stream_per_sub_batch) {
+                         uint32_t sub_batches, bool stream_per_sub_batch, float loss_threshold) {
                  PipelineConfig c = kind == "hand" ? PipelineConfig::hand() : PipelineConfig::face();
                  if (kind != "hand" && kind != "face")
                      throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "pipeline kind must be 'face' or 'hand'");
                  c.max_rois_per_frame = max_rois;
                  c.sub_batches = sub_batches;
                  c.stream_per_sub_batch = stream_per_sub_batch;
+                 c.loss_threshold = loss_threshold;  // LandmarkTracker::set_loss_threshold
                  return new DetectTrackPipeline(c, device, threads);
              }), py::arg("kind") = "face", py::arg("device") = 0, py::arg("threads") = 8,
              py::arg("max_rois_per_frame") = 8, py::arg("sub_batches") = 2,
-             py::arg("stream_per_sub_batch") = true)
+             py::arg("stream_per_sub_batch") = true,
+             py::arg("loss_threshold") = LandmarkTracker::DEFAULT_LOSS_THRESHOLD)
         // frames: list of (device ptr, width, height, row_stride); forced: per frame list of
         // (cx, cy, w, h, rad) ROIs used when the frame has no detection
         .def("run", [](DetectTrackPipeline &p, const std::vector<std::tuple<uint64_t, uint32_t, uint32_t, uint64_t>> &frames,
@@ -353,6 +355,7 @@ PYBIND11_MODULE(_zaru_host, m) {
             d["frame"] = r.frame;
             d["from_detection"] = r.from_detection;
             d["tracked"] = r.tracked;
+            d["confidence"] = r.confidence;
             d["roi"] = r.roi;
             d["view_rect"] = r.result.view_rect;
             d["updated_roi"] = r.result.updated_roi;

@@ -320,9 +320,11 @@ void DetectTrackPipeline::stage_map(Slot &s) {
         Estimate e;
         extract_landmarks(cfg_.landmarker, outs, e);
         map_estimate(e, s.local_rect[i], lin_w);
+        r.confidence = e.confidence;
         r.tracked = tracker_update(cfg_.landmarker, r.roi, r.result.view_rect, cfg_.loss_threshold,
                                    cfg_.roi_padding, e, r.result, r.next_roi);
-        if (!r.tracked) r.result.estimate = std::move(e);
+        // lost: LandmarkTracker::track returns None (landmark.rs:468-477) -- no landmarks are
+        // published, in particular not the view-local ones of the discarded estimate
     });
 }
 

@@ -39,9 +39,12 @@ struct RoiResult {
     uint32_t frame = 0;
     bool from_detection = false;
     bool tracked = false;  // false: confidence below the loss threshold
+    float confidence = 0.f;  // the estimate's Confidence (face_flag / hand presence), always set
     RotatedRect roi;       // ROI the tracker was seeded with
-    TrackingResult result; // valid when tracked
-    RotatedRect next_roi;
+    // tracked: landmarks in frame coordinates, view/updated ROI.  Lost: the reference returns
+    // None (landmark.rs:468-477), so only view_rect is set and the estimate stays empty.
+    TrackingResult result;
+    RotatedRect next_roi;  // valid when tracked
 };
 
 struct StageTimes {  // mirrors Detector::timers / Estimator::timers (detection.rs:273-275)
