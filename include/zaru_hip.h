@@ -7,7 +7,8 @@
  *   - every call returns ZR_OK (0) or a negative error class and sets a thread-local message
  *     readable with zr_last_error() (reference: anyhow::Error from Loader::load /
  *     NeuralNetwork::estimate, crates/zaru/src/nn/mod.rs:259, 450);
- *   - no C++ exception or abort crosses this boundary;
+ *   - no C++ exception or abort crosses this boundary: every entry point catches at the
+ *     boundary (host out-of-memory -> ZR_ERR_DEVICE, anything else -> ZR_ERR_INTERNAL);
  *   - a session is safe to use from several threads at once (NeuralNetwork is Clone + Send +
  *     Sync and HandTracker workers call estimate(&self) concurrently,
  *     crates/zaru/src/hand/tracking.rs:165-181);
@@ -31,6 +32,7 @@ extern "C" {
 #define ZR_ERR_MODEL (-2)       /* malformed ONNX, or an operator/pattern with no HIP lowering */
 #define ZR_ERR_DEVICE (-3)      /* HIP runtime failure (no GPU, out of memory, ...) */
 #define ZR_ERR_SHAPE (-4)       /* tensor count or shape mismatch */
+#define ZR_ERR_INTERNAL (-5)    /* unexpected internal failure (caught at the boundary) */
 
 typedef struct zr_session zr_session; /* = Arc<NeuralNetworkImpl> (crates/zaru/src/nn/mod.rs:369-375) */
 

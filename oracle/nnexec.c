@@ -105,7 +105,7 @@ typedef struct {
 static void pb_attr_parse(pb_slice b, pb_attr *a) {
     memset(a, 0, sizeof(*a));
     a->raw = b;
-    pb_field f;
+    pb_field f = {0};
     while (pb_next(&b, &f)) {
         if (f.field == 1 && f.wire == 2) {
             a->name = (const char *)f.bytes.p;
@@ -124,7 +124,7 @@ static void pb_attr_parse(pb_slice b, pb_attr *a) {
 
 static int pb_attr_ints(const pb_attr *a, int64_t *out, int cap) {
     pb_slice b = a->raw;
-    pb_field f;
+    pb_field f = {0};
     int n = 0;
     while (pb_next(&b, &f)) {
         if (f.field != 8) continue;
@@ -166,7 +166,7 @@ typedef struct {
 
 static void parse_tensor(pb_slice b, raw_tensor *t) {
     memset(t, 0, sizeof(*t));
-    pb_field f;
+    pb_field f = {0};
     while (pb_next(&b, &f)) {
         if (f.field == 1) {
             if (f.wire == 0) t->dims[t->ndim++] = (int64_t)f.v;
@@ -193,7 +193,7 @@ struct zo_net {
     static struct net_s_##SUF *load_##SUF(const uint8_t *bytes, size_t len) {                   \
         struct net_s_##SUF *n = (struct net_s_##SUF *)calloc(1, sizeof(*n));                    \
         pb_slice m = {bytes, len}, g = {NULL, 0};                                               \
-        pb_field f;                                                                             \
+        pb_field f = {0};                                                                             \
         while (pb_next(&m, &f))                                                                 \
             if (f.field == 7 && f.wire == 2) g = f.bytes;                                       \
         if (!g.p) {                                                                             \
@@ -212,7 +212,7 @@ struct zo_net {
                 nd->in = (char **)calloc(16, sizeof(char *));                                   \
                 nd->out = (char **)calloc(8, sizeof(char *));                                   \
                 pb_slice ns = f.bytes;                                                          \
-                pb_field g2;                                                                    \
+                pb_field g2 = {0};                                                                    \
                 while (pb_next(&ns, &g2)) {                                                     \
                     if (g2.field == 1) nd->in[nd->nin++] = pb_str(g2.bytes);                    \
                     else if (g2.field == 2) nd->out[nd->nout++] = pb_str(g2.bytes);             \
@@ -251,24 +251,24 @@ struct zo_net {
                 free(rt.name);                                                                  \
             } else if (f.field == 11 && !n->input_name) {                                       \
                 pb_slice vi = f.bytes;                                                          \
-                pb_field g2;                                                                    \
+                pb_field g2 = {0};                                                                    \
                 while (pb_next(&vi, &g2)) {                                                     \
                     if (g2.field == 1) n->input_name = pb_str(g2.bytes);                        \
                     else if (g2.field == 2) { /* TypeProto.tensor_type.shape.dim */             \
                         pb_slice tp = g2.bytes;                                                 \
-                        pb_field g3;                                                            \
+                        pb_field g3 = {0};                                                            \
                         while (pb_next(&tp, &g3)) {                                             \
                             if (g3.field != 1) continue;                                        \
                             pb_slice tt = g3.bytes;                                             \
-                            pb_field g4;                                                        \
+                            pb_field g4 = {0};                                                        \
                             while (pb_next(&tt, &g4)) {                                         \
                                 if (g4.field != 2) continue;                                    \
                                 pb_slice sh = g4.bytes;                                         \
-                                pb_field g5;                                                    \
+                                pb_field g5 = {0};                                                    \
                                 int d = 0;                                                      \
                                 while (pb_next(&sh, &g5)) {                                     \
                                     pb_slice dm = g5.bytes;                                     \
-                                    pb_field g6;                                                \
+                                    pb_field g6 = {0};                                                \
                                     while (pb_next(&dm, &g6))                                   \
                                         if (g6.field == 1 && d < 4)                             \
                                             n->input_dims[d] = (int64_t)g6.v;                   \
@@ -280,7 +280,7 @@ struct zo_net {
                 }                                                                               \
             } else if (f.field == 12 && n->noutputs < 8) {                                      \
                 pb_slice vi = f.bytes;                                                          \
-                pb_field g2;                                                                    \
+                pb_field g2 = {0};                                                                    \
                 while (pb_next(&vi, &g2))                                                       \
                     if (g2.field == 1) n->outputs[n->noutputs++] = pb_str(g2.bytes);            \
             }                                                                                   \

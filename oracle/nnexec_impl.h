@@ -120,26 +120,49 @@ static int NN(op_conv)(struct NN(net_s) *n, const NN(node) *nd) {
     int64_t od[4] = {1, M, OH, OW};
     NN(tensor) *y = NN(new_out)(n, nd->out[0], 4, od);
     int64_t mg = M / g;
+    /* Every output starts at its bias and accumulates w * x over (c, ky, kx) in ascending
+     * order, skipping taps outside the input -- the ONNX Conv definition evaluated term by
+     * term.  The loops run tap-major with the output row innermost (vectorisable), which
+     * keeps exactly that per-output summation order. */
     for (int64_t m = 0; m < M; m++) {
+        REAL *ym = y->f + m * OH * OW;
+        const REAL bm = b ? b->f[m] : (REAL)0;
+        for (int64_t p = 0; p < OH * OW; p++) ym[p] = bm;
         int64_t grp = m / mg;
-        for (int64_t oy = 0; oy < OH; oy++)
-            for (int64_t ox = 0; ox < OW; ox++) {
-                REAL acc = b ? b->f[m] : (REAL)0;
-                for (int64_t c = 0; c < CG; c++) {
-                    int64_t ic = grp * CG + c;
-                    for (int64_t ky = 0; ky < KH; ky++) {
-                        int64_t iy = oy * st[0] - pads[0] + ky * dil[0];
-                        if (iy < 0 || iy >= H) continue;
-                        for (int64_t kx = 0; kx < KW; kx++) {
-                            int64_t ix = ox * st[1] - pads[1] + kx * dil[1];
-                            if (ix < 0 || ix >= W) continue;
-                            acc += w->f[((m * CG + c) * KH + ky) * KW + kx] *
-                                   x->f[(ic * H + iy) * W + ix];
-                        }
+        if (KH == 1 && KW == 1 && st[0] == 1 && st[1] == 1 && !pads[0] && !pads[1] && !pads[2] &&
+            !pads[3]) { /* 1x1: one contiguous axpy per input channel */
+            for (int64_t c = 0; c < CG; c++) {
+                const REAL wv = w->f[m * CG + c], *xc = x->f + (grp * CG + c) * H * W;
+                for (int64_t p = 0; p < OH * OW; p++) ym[p] += wv * xc[p];
+            }
+            continue;
+        }
+        for (int64_t c = 0; c < CG; c++) {
+            int64_t ic = grp * CG + c;
+            const REAL *xc = x->f + ic * H * W;
+            for (int64_t ky = 0; ky < KH; ky++) {
+                /* oy with 0 <= oy*st0 - pad0 + ky*dil0 < H */
+                int64_t a = pads[0] - ky * dil[0];
+                int64_t oy0 = a <= 0 ? 0 : (a + st[0] - 1) / st[0];
+                int64_t oy1 = H - 1 + a < 0 ? -1 : (H - 1 + a) / st[0];
+                if (oy1 > OH - 1) oy1 = OH - 1;
+                for (int64_t kx = 0; kx < KW; kx++) {
+                    const REAL wv = w->f[((m * CG + c) * KH + ky) * KW + kx];
+                    int64_t bx = pads[1] - kx * dil[1];
+                    int64_t ox0 = bx <= 0 ? 0 : (bx + st[1] - 1) / st[1];
+                    int64_t ox1 = W - 1 + bx < 0 ? -1 : (W - 1 + bx) / st[1];
+                    if (ox1 > OW - 1) ox1 = OW - 1;
+                    for (int64_t oy = oy0; oy <= oy1; oy++) {
+                        const REAL *xr = xc + (oy * st[0] - a) * W - bx;
+                        REAL *yr = ym + oy * OW;
+                        if (st[1] == 1)
+                            for (int64_t ox = ox0; ox <= ox1; ox++) yr[ox] += wv * xr[ox];
+                        else
+                            for (int64_t ox = ox0; ox <= ox1; ox++) yr[ox] += wv * xr[ox * st[1]];
                     }
                 }
-                y->f[(m * OH + oy) * OW + ox] = acc;
             }
+        }
     }
     return 0;
 }

@@ -62,3 +62,88 @@ def test_unsupported_operator_is_an_error(models_dir):
     with pytest.raises(_lib.ZaruError) as e:
         _lib.plan_describe(model)
     assert e.value.code == -2 and "Softmax" in str(e.value)
+
+
+# ---------------------------------------------------------------- untrusted ONNX input
+# A minimal ModelProto (one 1x1 Conv, x[1,3,8,8] -> y) written with the protobuf wire
+# format, then corrupted one field at a time: every variant must come back as a model error
+# (zr_plan_describe parses and compiles like zr_session_create, without a GPU), never a crash
+# or an over-read.
+def _varint(v):
+    out = bytearray()
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        out.append(b | (0x80 if v else 0))
+        if not v:
+            return bytes(out)
+
+
+def _fld(num, payload):
+    return _varint((num << 3) | 2) + _varint(len(payload)) + payload
+
+
+def _vfld(num, v):
+    return _varint(num << 3) + _varint(v & ((1 << 64) - 1))
+
+
+def _tensor(name, dims, dtype, raw):
+    return b"".join(_vfld(1, d) for d in dims) + _vfld(2, dtype) + _fld(8, name) + _fld(9, raw)
+
+
+def _value_info(name, dims):
+    shape = b"".join(_fld(1, _vfld(1, d)) for d in dims)
+    return _fld(1, name) + _fld(2, _fld(1, _vfld(1, 1) + _fld(2, shape)))
+
+
+def _model(w_tensor, strides=(1, 1)):
+    attr = _fld(1, b"strides") + b"".join(_vfld(8, s) for s in strides) + _vfld(20, 7)
+    # NodeProto: inputs = field 1 repeated (x, w), output = field 2 (y), op_type = field 4
+    node = _fld(1, b"x") + _fld(1, b"w") + _fld(2, b"y") + _fld(4, b"Conv") + _fld(5, attr)
+    graph = (_fld(1, node) + _fld(5, w_tensor) + _fld(11, _value_info(b"x", [1, 3, 8, 8])) +
+             _fld(12, _value_info(b"y", [1, 4, 8, 8])))
+    return _fld(7, graph)
+
+
+def _w(dims=(4, 3, 1, 1), dtype=1, nbytes=None):
+    import numpy as np
+    n = int(np.prod(dims)) if dims else 1
+    size = {1: 4, 6: 4, 7: 8, 10: 2}[dtype]
+    raw = b"\x00" * (n * size if nbytes is None else nbytes)
+    return _tensor(b"w", dims, dtype, raw)
+
+
+def test_minimal_model_compiles():
+    txt = _lib.plan_describe(_model(_w()))
+    assert "gemm" in txt.splitlines()[-1]
+
+
+@pytest.mark.parametrize("case", ["truncated", "raw_short", "raw_long", "fp16_short",
+                                  "int32_short", "int64_short", "negative_dim", "huge_dims",
+                                  "zero_stride", "double_weights", "wrong_rank"])
+def test_malformed_tensor_is_a_model_error(case):
+    if case == "truncated":
+        m = _model(_w())[:-7]
+    elif case == "raw_short":
+        m = _model(_w(nbytes=47))
+    elif case == "raw_long":
+        m = _model(_w(nbytes=4 * 12 + 4))
+    elif case == "fp16_short":
+        m = _model(_w(dtype=10, nbytes=23))
+    elif case == "int32_short":
+        m = _model(_w(dtype=6, nbytes=5))
+    elif case == "int64_short":
+        m = _model(_w(dtype=7, nbytes=9))
+    elif case == "negative_dim":
+        m = _model(_tensor(b"w", [4, -3, 1, 1], 1, b""))
+    elif case == "huge_dims":  # numel overflows int64 without the bound
+        m = _model(_tensor(b"w", [1 << 40, 1 << 40, 1, 1], 1, b"\x00" * 16))
+    elif case == "zero_stride":
+        m = _model(_w(), strides=(0, 1))
+    elif case == "double_weights":  # dtype 11 carries no f32 data
+        m = _model(_tensor(b"w", [4, 3, 1, 1], 11, b"\x00" * 96))
+    else:
+        m = _model(_w(dims=(4, 3)))
+    with pytest.raises(_lib.ZaruError) as e:
+        _lib.plan_describe(m)
+    assert e.value.code == -2, str(e.value)

@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(LIB_DIR, "libzaru_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "zaru_hip.h")
 
 ZR_OK = 0
-ERRORS = {-1: "invalid argument", -2: "model", -3: "device", -4: "shape"}
+ERRORS = {-1: "invalid argument", -2: "model", -3: "device", -4: "shape", -5: "internal"}
 
 
 class ZaruError(RuntimeError):

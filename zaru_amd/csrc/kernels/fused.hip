@@ -108,10 +108,7 @@ static const char *stem_go(const StemParams &p, bool pre, hipStream_t s) {
     dim3 grid(tiles, p.N);
     if (pre) hipLaunchKernelGGL((stem_kernel<K, S, CO, true>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((stem_kernel<K, S, CO, false>), grid, dim3(256), 0, s, p);
-    static char names[2][2][3][2][40];
-    char *nm = names[K == 5][S == 2][CO / 8 - 2][pre];
-    if (!nm[0]) snprintf(nm, 40, "stem_kernel<%d,%d,%d,%s>", K, S, CO, pre ? "true" : "false");
-    return nm;
+    return kernel_name("stem_kernel<%d,%d,%d,%s>", K, S, CO, pre ? "true" : "false");
 }
 
 template <int K, int S>
@@ -1003,26 +1000,17 @@ const char *dwpw_go(const DwPwParams &p, hipStream_t s) {
         if (fkc == 32) {
             if (const size_t lds = dma_plan<K, S, WM, MTW, 32>(p, &runmax, &bufsz)) {
                 hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, 32>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
-                static char dn[2][2][5][5][48];
-                char *nm = dn[K == 5][S == 2][WM][MTW];
-                if (!nm[0]) snprintf(nm, 48, "dwpw_dma_kernel<%d,%d,%d,%d,32>", K, S, WM, MTW);
-                return nm;
+                return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,32>", K, S, WM, MTW);
             }
         } else if (const size_t lds = dma_plan<K, S, WM, MTW, 16>(p, &runmax, &bufsz)) {
             hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, 16>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
-            static char dn[2][2][5][5][48];
-            char *nm = dn[K == 5][S == 2][WM][MTW];
-            if (!nm[0]) snprintf(nm, 48, "dwpw_dma_kernel<%d,%d,%d,%d,16>", K, S, WM, MTW);
-            return nm;
+            return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,16>", K, S, WM, MTW);
         }
     }
     const bool v4 = v4_ok(p);
     if (v4) hipLaunchKernelGGL((dwpw_kernel<K, S, WM, MTW, 1, true>), grid, dim3(256), 0, s, p, nct);
     else hipLaunchKernelGGL((dwpw_kernel<K, S, WM, MTW, 1, false>), grid, dim3(256), 0, s, p, nct);
-    static char names[2][2][5][5][2][48];  // the symbol as rocprofv3 prints it, spaces removed
-    char *nm = names[K == 5][S == 2][WM][MTW][v4];
-    if (!nm[0]) snprintf(nm, 48, "dwpw_kernel<%d,%d,%d,%d,1,%s>", K, S, WM, MTW, v4 ? "true" : "false");
-    return nm;
+    return kernel_name("dwpw_kernel<%d,%d,%d,%d,1,%s>", K, S, WM, MTW, v4 ? "true" : "false");
 }
 
 template <int K, int S>
@@ -1057,10 +1045,7 @@ const char *dwpw_rows_go(const DwPwParams &p, hipStream_t s) {
     const size_t lds = sizeof(float) * ((size_t)RFKC * rmax * Wp + RFKC * RBN + RFKC * MT * 32);
     dim3 grid((ntiles + 7) / 8 * 8);
     hipLaunchKernelGGL((dwpw_rows_kernel<K, S, MT>), grid, dim3(256), lds, s, p, tpi, ntiles, rmax);
-    static char names[2][2][4][48];
-    char *nm = names[K == 5][S == 2][MT];
-    if (!nm[0]) snprintf(nm, 48, "dwpw_rows_kernel<%d,%d,%d>", K, S, MT);
-    return nm;
+    return kernel_name("dwpw_rows_kernel<%d,%d,%d>", K, S, MT);
 }
 
 template <int K, int S>
@@ -1108,11 +1093,8 @@ const char *dwpw_valu_go(const DwPwParams &p, hipStream_t s) {
         const size_t lds = sizeof(float) * (size_t)VFKC * rmax * lw;
         hipLaunchKernelGGL((dwpw_valu_kernel<K, S, CO, false, VFKC>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
     }
-    static char names[2][2][5][2][2][56];
     const int vfe = db ? vf : VFKC;
-    char *nm = names[K == 5][S == 2][CO / 16][db][vfe == 4];
-    if (!nm[0]) snprintf(nm, 56, "dwpw_valu_kernel<%d,%d,%d,%s,%d>", K, S, CO, db ? "true" : "false", vfe);
-    return nm;
+    return kernel_name("dwpw_valu_kernel<%d,%d,%d,%s,%d>", K, S, CO, db ? "true" : "false", vfe);
 }
 
 template <int K, int S>
@@ -1134,10 +1116,7 @@ const char *dwpw_img_go(const DwPwParams &p, hipStream_t s) {
     const size_t lds = sizeof(float) * ((size_t)IFKC * G * Hp * Wp + IFKC * IBN + IFKC * MT * 32);
     dim3 grid((ntiles + 7) / 8 * 8, mb);
     hipLaunchKernelGGL((dwpw_img_kernel<K, S, MT, NTW>), grid, dim3(256), lds, s, p, G, ntiles, nimg);
-    static char names[2][2][5][48];
-    char *nm = names[K == 5][S == 2][MT];
-    if (!nm[0]) snprintf(nm, 48, "dwpw_img_kernel<%d,%d,%d,%d>", K, S, MT, NTW);
-    return nm;
+    return kernel_name("dwpw_img_kernel<%d,%d,%d,%d>", K, S, MT, NTW);
 }
 
 template <int K, int S>

@@ -2,10 +2,27 @@
 // folded into a GEMM epilogue): standalone activation / Add / MaxPool 2x2 / channel Pad,
 // bilinear Resize (half_pixel, palm FPN), GlobalAveragePool (hand head), plus the detector
 // candidate compaction that keeps the bit-exact decode on the host cheap.
+#include <cstdarg>
+#include <cstdio>
+#include <mutex>
+#include <set>
+#include <string>
 #include "../runtime/zr_kernels.h"
 #include "act.h"
 
 namespace zr {
+
+const char *kernel_name(const char *fmt, ...) {
+    char buf[128];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    static std::mutex mu;
+    static std::set<std::string> names;
+    std::lock_guard<std::mutex> g(mu);
+    return names.insert(buf).first->c_str();
+}
 
 __device__ __forceinline__ const float *plane_ptr(const Plane &p, int n, int c) {
     return p.p + (int64_t)n * p.sN + (int64_t)c * p.sC;

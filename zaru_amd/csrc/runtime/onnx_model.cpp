@@ -139,47 +139,60 @@ bool parse_tensor(Reader r, std::string &name, OnnxTensor &t, std::string &err) 
         err = "malformed TensorProto";
         return false;
     }
-    const int64_t n = t.numel();
+    // untrusted dims: each >= 0 and the product bounded before anything is sized from it
+    int64_t n = 1;
+    for (int64_t d : t.dims) {
+        if (d < 0 || (d > 0 && n > OnnxTensor::kMaxTensorElems / d))
+            return err = "tensor " + name + ": negative or oversized dims", false;
+        n *= d;
+    }
+    auto need = [&](size_t have, int64_t elem, const char *what) {
+        if ((uint64_t)have != (uint64_t)n * (uint64_t)elem) {
+            err = std::string(what) + " size mismatch for " + name;
+            return false;
+        }
+        return true;
+    };
     if (t.dtype == 1) {
         if (raw) {
-            if ((int64_t)raw_len != n * 4) return err = "raw_data size mismatch for " + name, false;
-            t.f.resize(n);
+            if (!need(raw_len, 4, "float raw_data")) return false;
+            t.f.resize((size_t)n);
             memcpy(t.f.data(), raw, raw_len);
         } else {
-            if ((int64_t)fdata.size() != n) return err = "float_data size mismatch for " + name, false;
+            if (!need(fdata.size(), 1, "float_data")) return false;
             t.f = std::move(fdata);
         }
     } else if (t.dtype == 10) {
-        t.f.resize(n);
-        if (raw) {
-            if ((int64_t)raw_len != n * 2) return err = "fp16 size mismatch for " + name, false;
-            for (int64_t i = 0; i < n; i++) {
-                uint16_t h;
-                memcpy(&h, raw + 2 * i, 2);
-                t.f[i] = half_to_float(h);
-            }
-        } else {
-            if ((int64_t)i32data.size() != n) return err = "fp16 data size mismatch", false;
-            for (int64_t i = 0; i < n; i++) t.f[i] = half_to_float((uint16_t)i32data[i]);
+        if (raw ? !need(raw_len, 2, "float16 raw_data") : !need(i32data.size(), 1, "float16 int32_data"))
+            return false;
+        t.f.resize((size_t)n);
+        for (int64_t i = 0; i < n; i++) {
+            uint16_t h;
+            if (raw) memcpy(&h, raw + 2 * i, 2);
+            else h = (uint16_t)i32data[i];
+            t.f[i] = half_to_float(h);
         }
         t.dtype = 1;
     } else if (t.dtype == 7) {
         if (raw) {
-            if ((int64_t)raw_len != n * 8) return err = "int64 raw size mismatch", false;
-            t.i64.resize(n);
+            if (!need(raw_len, 8, "int64 raw_data")) return false;
+            t.i64.resize((size_t)n);
             memcpy(t.i64.data(), raw, raw_len);
         } else {
+            if (!need(idata.size(), 1, "int64_data")) return false;
             t.i64 = std::move(idata);
         }
     } else if (t.dtype == 6) {  // int32 -> int64
         if (raw) {
-            t.i64.resize(n);
+            if (!need(raw_len, 4, "int32 raw_data")) return false;
+            t.i64.resize((size_t)n);
             for (int64_t i = 0; i < n; i++) {
                 int32_t v;
                 memcpy(&v, raw + 4 * i, 4);
                 t.i64[i] = v;
             }
         } else {
+            if (!need(i32data.size(), 1, "int32_data")) return false;
             t.i64 = std::move(i32data);
         }
         t.dtype = 7;

@@ -51,11 +51,14 @@ struct OnnxTensor {
     int dtype = 0;             // TensorProto.DataType: 1 float, 7 int64, 10 float16
     std::vector<float> f;      // float / float16 data (converted to f32)
     std::vector<int64_t> i64;  // int64 data
+    // element count; only meaningful after parse_tensor validated the dims (each >= 0, product
+    // <= kMaxTensorElems), so it cannot overflow
     int64_t numel() const {
         int64_t n = 1;
         for (auto d : dims) n *= d;
         return n;
     }
+    static constexpr int64_t kMaxTensorElems = int64_t(1) << 30;  // 4 GiB of f32
 };
 
 struct OnnxValueInfo {

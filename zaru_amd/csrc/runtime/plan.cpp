@@ -90,21 +90,56 @@ bool Compiler::infer_shapes() {
         if (!v.shape.empty() && v.shape[0] <= 0) v.shape[0] = 1;
         v.is_input = true;
     }
-    for (auto &kv : M.inits) val(kv.first).shape = kv.second.dims;
+    for (auto &kv : M.inits) {
+        // a float initializer must carry exactly numel values (the parser checked the raw
+        // sizes; this also rejects dtypes that carry no f32 data, e.g. double weights)
+        const OnnxTensor &t = kv.second;
+        if (t.dtype == 1 && (int64_t)t.f.size() != t.numel()) return fail("initializer " + kv.first + ": no f32 data");
+        val(kv.first).shape = t.dims;
+    }
+    for (auto &vi : M.inputs)
+        for (size_t i = 1; i < vi.dims.size(); i++)
+            if (vi.dims[i] <= 0 || vi.dims[i] > (1 << 16)) return fail("graph input " + vi.name + ": bad dims");
+    // f32 weight operand with exactly the expected rank
+    auto weight = [&](const std::string &n, size_t rank) -> const OnnxTensor * {
+        const OnnxTensor *t = init(n);
+        if (!t || t->dtype != 1 || t->dims.size() != rank) return nullptr;
+        for (auto d : t->dims)
+            if (d <= 0) return nullptr;
+        return t;
+    };
     for (size_t ni = 0; ni < M.nodes.size(); ni++) {
         const OnnxNode &nd = M.nodes[ni];
+        const std::string &op = nd.op;
+        // operand arity, and every operand must be a known value (graph input, initializer or
+        // an earlier node's output: ONNX graphs are topologically sorted)
+        const size_t arity = (op == "Conv" || op == "Add" || op == "PRelu" || op == "Gemm" ||
+                              op == "Reshape") ? 2 : 1;
+        if (nd.in.size() < arity || nd.out.empty() || nd.in[0].empty())
+            return fail(op + " " + nd.name + ": missing operands");
+        for (auto &i : nd.in)
+            if (!i.empty() && !init(i) && (!vals.count(i) || vals[i].shape.empty()))
+                return fail(op + " " + nd.name + ": operand " + i + " is not defined before use");
         for (auto &o : nd.out) producer[o] = (int)ni;
         for (auto &i : nd.in)
             if (!i.empty()) vals[i].consumers++;
         auto in = [&](int k) -> std::vector<int64_t> & { return val(nd.in[k]).shape; };
         std::vector<int64_t> s;
-        const std::string &op = nd.op;
         if (op == "Conv") {
             auto &x = in(0);
-            const OnnxTensor *w = init(nd.in[1]);
-            if (!w || x.size() != 4 || w->dims.size() != 4) return fail("Conv " + nd.name + ": unsupported operands");
+            const OnnxTensor *w = weight(nd.in[1], 4);
+            if (!w || x.size() != 4) return fail("Conv " + nd.name + ": unsupported operands");
             auto st = nd.getints("strides", {1, 1});
             auto pads = nd.getints("pads", {0, 0, 0, 0});
+            const int64_t g = nd.geti("group", 1);
+            if (st.size() != 2 || st[0] <= 0 || st[1] <= 0 || pads.size() != 4 ||
+                *std::min_element(pads.begin(), pads.end()) < 0 || g <= 0 || x[1] != w->dims[1] * g ||
+                w->dims[0] % g)
+                return fail("Conv " + nd.name + ": bad strides/pads/group");
+            if (nd.in.size() > 2 && !nd.in[2].empty()) {
+                const OnnxTensor *b = weight(nd.in[2], 1);
+                if (!b || b->dims[0] != w->dims[0]) return fail("Conv " + nd.name + ": bias shape");
+            }
             if (nd.gets("auto_pad", "NOTSET") != "NOTSET") return fail("Conv auto_pad unsupported");
             int64_t oh = (x[2] + pads[0] + pads[2] - w->dims[2]) / st[0] + 1;
             int64_t ow = (x[3] + pads[1] + pads[3] - w->dims[3]) / st[1] + 1;
@@ -117,7 +152,8 @@ bool Compiler::infer_shapes() {
             auto k = nd.getints("kernel_shape");
             auto st = nd.getints("strides", {1, 1});
             auto pads = nd.getints("pads", {0, 0, 0, 0});
-            if (k.size() != 2) return fail("MaxPool kernel_shape");
+            if (k.size() != 2 || st.size() != 2 || st[0] <= 0 || st[1] <= 0 || pads.size() != 4 || x.size() != 4)
+                return fail("MaxPool kernel_shape/strides/pads");
             s = {x[0], x[1], (x[2] + pads[0] + pads[2] - k[0]) / st[0] + 1,
                  (x[3] + pads[1] + pads[3] - k[1]) / st[1] + 1};
         } else if (op == "Pad") {
@@ -136,8 +172,10 @@ bool Compiler::infer_shapes() {
             auto &x = in(0);
             const OnnxTensor *sz = nd.in.size() > 3 && !nd.in[3].empty() ? init(nd.in[3]) : nullptr;
             const OnnxTensor *sc = nd.in.size() > 2 && !nd.in[2].empty() ? init(nd.in[2]) : nullptr;
+            if (x.size() != 4) return fail("Resize of a non-4D tensor");
             if (sz && sz->i64.size() == 4) s = sz->i64;
-            else if (sc && sc->f.size() == 4)
+            else if (sc && sc->f.size() == 4 && sc->f[2] > 0.f && sc->f[3] > 0.f && sc->f[2] <= 64.f &&
+                     sc->f[3] <= 64.f)
                 s = {x[0], x[1], (int64_t)std::floor(x[2] * sc->f[2]), (int64_t)std::floor(x[3] * sc->f[3])};
             else return fail("Resize needs constant sizes or scales");
         } else if (op == "GlobalAveragePool") {
@@ -164,32 +202,62 @@ bool Compiler::infer_shapes() {
             int64_t known = 1;
             int neg = -1;
             for (size_t i = 0; i < t->i64.size(); i++) {
+                if (t->i64[i] == 0 && i >= x.size()) return fail("Reshape copies a missing dim");
                 int64_t d = t->i64[i] == 0 ? x[i] : t->i64[i];
-                if (d == -1) neg = (int)i;
+                if (d == -1 && neg < 0) neg = (int)i;
+                else if (d <= 0) return fail("Reshape dims");
                 else known *= d;
                 s.push_back(d);
             }
             int64_t total = 1;
             for (auto d : x) total *= d;
             if (neg >= 0) s[neg] = total / known;
+            int64_t got = 1;
+            for (auto d : s) got *= d;
+            if (got != total) return fail("Reshape changes the element count");
         } else if (op == "Transpose") {
             auto &x = in(0);
             auto perm = nd.getints("perm");
             if (perm.size() != x.size()) return fail("Transpose perm");
-            for (auto p : perm) s.push_back(x[p]);
+            for (auto p : perm) {
+                if (p < 0 || p >= (int64_t)x.size()) return fail("Transpose perm");
+                s.push_back(x[p]);
+            }
         } else if (op == "Concat") {
             s = in(0);
             int64_t ax = nd.geti("axis", 0);
             if (ax < 0) ax += (int64_t)s.size();
-            for (size_t k = 1; k < nd.in.size(); k++) s[ax] += in((int)k)[ax];
+            if (ax < 0 || ax >= (int64_t)s.size()) return fail("Concat axis");
+            for (size_t k = 1; k < nd.in.size(); k++) {
+                if (nd.in[k].empty() || in((int)k).size() != s.size()) return fail("Concat operands");
+                s[ax] += in((int)k)[ax];
+            }
         } else if (op == "Gemm") {
             auto &a = in(0);
-            const OnnxTensor *b = init(nd.in[1]);
+            const OnnxTensor *b = weight(nd.in[1], 2);
             if (!b || a.size() != 2) return fail("Gemm operands");
-            int64_t m = nd.geti("transB", 0) ? b->dims[0] : b->dims[1];
+            const bool tb = nd.geti("transB", 0) != 0;
+            if (a[1] != (tb ? b->dims[1] : b->dims[0])) return fail("Gemm K mismatch");
+            int64_t m = tb ? b->dims[0] : b->dims[1];
+            if (nd.in.size() > 2 && !nd.in[2].empty()) {
+                const OnnxTensor *c = init(nd.in[2]);
+                if (!c || c->dtype != 1 || (c->f.size() != 1 && (int64_t)c->f.size() != m))
+                    return fail("Gemm bias shape");
+            }
             s = {a[0], m};
         } else {
             return fail("unsupported operator " + op + " (" + nd.name + ")");
+        }
+        // every produced shape: positive dims, bounded per-image size (kernels address with
+        // 32-bit element offsets)
+        if (s.empty()) return fail(op + " " + nd.name + ": empty shape");
+        int64_t pi = 1;
+        for (size_t i = 0; i < s.size(); i++) {
+            if (s[i] <= 0 || s[i] > (1 << 24)) return fail(op + " " + nd.name + ": bad output shape");
+            if (i > 0) {
+                pi *= s[i];
+                if (pi > (int64_t(1) << 28)) return fail(op + " " + nd.name + ": tensor too large");
+            }
         }
         for (auto &o : nd.out) val(o).shape = s;
     }
@@ -599,6 +667,7 @@ bool Compiler::lower() {
             auto &xs = val(nd.in[0]).shape, &ys = val(nd.out[0]).shape;
             std::vector<int64_t> pads = nd.in.size() > 1 && !nd.in[1].empty() ? init(nd.in[1])->i64
                                                                               : nd.getints("pads");
+            if (pads.size() != 8) return fail("Pad rank");
             const std::string mode = nd.gets("mode", "constant");
             float cval = 0.f;
             if (nd.in.size() > 2 && !nd.in[2].empty()) {

@@ -5,6 +5,7 @@
 
 #include <cmath>
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -20,9 +21,29 @@ namespace {
 
 thread_local std::string g_err;
 
-int set_err(int code, const std::string &msg) {
-    g_err = msg;
+int set_err(int code, const std::string &msg) noexcept {
+    try {
+        g_err = msg;
+    } catch (...) {  // out of memory for the message: keep the code, drop the text
+    }
     return code;
+}
+
+// Every extern "C" entry point runs its body through this: no C++ exception crosses the C
+// boundary (zaru_hip.h; a throw into the Rust caller's FFI frame is undefined behaviour).
+// std::bad_alloc (host allocations: pools, staging vectors, strings) maps to ZR_ERR_DEVICE's
+// "out of memory" class, anything else to ZR_ERR_INTERNAL.
+template <class F>
+int guarded(F &&body) noexcept {
+    try {
+        return body();
+    } catch (const std::bad_alloc &) {
+        return set_err(ZR_ERR_DEVICE, "out of host memory");
+    } catch (const std::exception &e) {
+        return set_err(ZR_ERR_INTERNAL, std::string("internal error: ") + e.what());
+    } catch (...) {
+        return set_err(ZR_ERR_INTERNAL, "internal error: unknown exception");
+    }
 }
 
 #define HIP_TRY(expr)                                                                    \
@@ -108,7 +129,7 @@ struct Profiler final : zr::LaunchHook {
         hipEvent_t a, b;
     };
     std::mutex mu;
-    bool on = false;
+    std::atomic<bool> on{false};  // read without the lock on the launch path
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
     hipEvent_t pending = nullptr;
@@ -220,9 +241,10 @@ int enqueue(zr_session *s, Ctx *c, int N, const float *input, int64_t in_sN, int
     b.weights = s->weights;
     b.pre = pre;
     {
+        const bool prof = s->prof.on.load();  // one read: the hook and its lock agree
         std::unique_lock<std::mutex> pl(s->prof.mu, std::defer_lock);
-        if (s->prof.on) pl.lock();
-        zr::run_plan(s->plan, b, stream, s->prof.on ? &s->prof : nullptr);
+        if (prof) pl.lock();
+        zr::run_plan(s->plan, b, stream, prof ? &s->prof : nullptr);
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->done, stream));
@@ -283,197 +305,215 @@ const char *zr_last_error(void) { return g_err.c_str(); }
 
 int zr_session_create(const uint8_t *onnx, size_t len, const uint32_t *out_sel, size_t n_sel,
                       int device, zr_session **out) {
-    if (!onnx || !out) return set_err(ZR_ERR_INVALID_ARGUMENT, "null model or out pointer");
-    *out = nullptr;
-    zr::OnnxModel m;
-    std::string err;
-    if (!zr::parse_onnx(onnx, len, m, err)) return set_err(ZR_ERR_MODEL, "ONNX parse error: " + err);
-    auto s = std::make_unique<zr_session>();
-    s->device = device;
-    std::vector<uint32_t> sel(out_sel, out_sel + n_sel);
-    if (!zr::compile_plan(m, sel, s->plan, err)) return set_err(ZR_ERR_MODEL, err);
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
-        return set_err(ZR_ERR_DEVICE, "no HIP device " + std::to_string(device));
-    HIP_TRY(hipSetDevice(device));
-    const size_t wb = s->plan.weights.size() * sizeof(float);
-    HIP_TRY(hipMalloc((void **)&s->weights, wb ? wb : 4));
-    HIP_TRY(hipMemcpy(s->weights, s->plan.weights.data(), wb, hipMemcpyHostToDevice));
-    *out = s.release();
-    return ZR_OK;
+    return guarded([&]() -> int {
+        if (!onnx || !out) return set_err(ZR_ERR_INVALID_ARGUMENT, "null model or out pointer");
+        *out = nullptr;
+        zr::OnnxModel m;
+        std::string err;
+        if (!zr::parse_onnx(onnx, len, m, err)) return set_err(ZR_ERR_MODEL, "ONNX parse error: " + err);
+        auto s = std::make_unique<zr_session>();
+        s->device = device;
+        std::vector<uint32_t> sel(out_sel, out_sel + n_sel);
+        if (!zr::compile_plan(m, sel, s->plan, err)) return set_err(ZR_ERR_MODEL, err);
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+            return set_err(ZR_ERR_DEVICE, "no HIP device " + std::to_string(device));
+        HIP_TRY(hipSetDevice(device));
+        const size_t wb = s->plan.weights.size() * sizeof(float);
+        HIP_TRY(hipMalloc((void **)&s->weights, wb ? wb : 4));
+        HIP_TRY(hipMemcpy(s->weights, s->plan.weights.data(), wb, hipMemcpyHostToDevice));
+        *out = s.release();
+        return ZR_OK;
+    });
 }
 
-void zr_session_destroy(zr_session *s) { delete s; }
+void zr_session_destroy(zr_session *s) { delete s; }  // destructors are noexcept
 
 int zr_session_num_io(const zr_session *s, int is_output, size_t *n) {
-    if (int rc = check_session(s)) return rc;
-    if (!n) return set_err(ZR_ERR_INVALID_ARGUMENT, "null n");
-    *n = is_output ? s->plan.outputs.size() : 1;
-    return ZR_OK;
+    return guarded([&]() -> int {
+        if (int rc = check_session(s)) return rc;
+        if (!n) return set_err(ZR_ERR_INVALID_ARGUMENT, "null n");
+        *n = is_output ? s->plan.outputs.size() : 1;
+        return ZR_OK;
+    });
 }
 
 int zr_session_io(const zr_session *s, int is_output, size_t idx, const char **name,
                   int64_t *shape, size_t *rank) {
-    if (int rc = check_session(s)) return rc;
-    if (!is_output) {
-        if (idx != 0) return set_err(ZR_ERR_INVALID_ARGUMENT, "input index out of range");
-        if (name) *name = s->plan.input_name.c_str();
-        if (shape) {
-            shape[0] = 1;
-            shape[1] = s->plan.in_C;
-            shape[2] = s->plan.in_H;
-            shape[3] = s->plan.in_W;
+    return guarded([&]() -> int {
+        if (int rc = check_session(s)) return rc;
+        if (!is_output) {
+            if (idx != 0) return set_err(ZR_ERR_INVALID_ARGUMENT, "input index out of range");
+            if (name) *name = s->plan.input_name.c_str();
+            if (shape) {
+                shape[0] = 1;
+                shape[1] = s->plan.in_C;
+                shape[2] = s->plan.in_H;
+                shape[3] = s->plan.in_W;
+            }
+            if (rank) *rank = 4;
+            return ZR_OK;
         }
-        if (rank) *rank = 4;
+        if (idx >= s->plan.outputs.size()) return set_err(ZR_ERR_INVALID_ARGUMENT, "output index out of range");
+        const auto &o = s->plan.outputs[idx];
+        if (name) *name = o.name.c_str();
+        if (shape)
+            for (size_t i = 0; i < o.shape.size() && i < 8; i++) shape[i] = i == 0 ? 1 : o.shape[i];
+        if (rank) *rank = o.shape.size();
         return ZR_OK;
-    }
-    if (idx >= s->plan.outputs.size()) return set_err(ZR_ERR_INVALID_ARGUMENT, "output index out of range");
-    const auto &o = s->plan.outputs[idx];
-    if (name) *name = o.name.c_str();
-    if (shape)
-        for (size_t i = 0; i < o.shape.size() && i < 8; i++) shape[i] = i == 0 ? 1 : o.shape[i];
-    if (rank) *rank = o.shape.size();
-    return ZR_OK;
+    });
 }
 
 int zr_plan_describe(const uint8_t *onnx, size_t len, const uint32_t *out_sel, size_t n_sel,
                      char *buf, size_t cap, size_t *needed) {
-    if (!onnx) return set_err(ZR_ERR_INVALID_ARGUMENT, "null model");
-    zr::OnnxModel m;
-    std::string err;
-    if (!zr::parse_onnx(onnx, len, m, err)) return set_err(ZR_ERR_MODEL, "ONNX parse error: " + err);
-    zr::Plan plan;
-    std::vector<uint32_t> sel(out_sel, out_sel + n_sel);
-    if (!zr::compile_plan(m, sel, plan, err)) return set_err(ZR_ERR_MODEL, err);
-    static const char *kinds[] = {"gemm", "dw", "direct", "elt", "resize", "gap", "dwpw"};
-    static const char *acts[] = {"none", "relu", "clip", "prelu", "sigmoid"};
-    std::string t;
-    char line[512];
-    auto ref = [](const zr::TRef &r) {
-        char b[96];
-        snprintf(b, sizeof b, "%s%d[%dx%dx%d]", r.kind == 0 ? "t" : r.kind == 1 ? "in" : "out",
-                 r.id, r.C, r.H, r.W);
-        return std::string(b);
-    };
-    snprintf(line, sizeof line, "input %s %dx%dx%d arena_per_image=%lld weights=%zu bytes/img=%.0f flops/img=%.0f fusable=%d\n",
-             plan.input_name.c_str(), plan.in_C, plan.in_H, plan.in_W,
-             (long long)plan.arena_per_image, plan.weights.size(), plan.bytes_per_image,
-             plan.flops_per_image, plan.input_fusable ? 1 : 0);
-    t += line;
-    for (auto &o : plan.outputs) {
-        snprintf(line, sizeof line, "output %s per_image=%lld\n", o.name.c_str(), (long long)o.per_image);
+    return guarded([&]() -> int {
+        if (!onnx) return set_err(ZR_ERR_INVALID_ARGUMENT, "null model");
+        zr::OnnxModel m;
+        std::string err;
+        if (!zr::parse_onnx(onnx, len, m, err)) return set_err(ZR_ERR_MODEL, "ONNX parse error: " + err);
+        zr::Plan plan;
+        std::vector<uint32_t> sel(out_sel, out_sel + n_sel);
+        if (!zr::compile_plan(m, sel, plan, err)) return set_err(ZR_ERR_MODEL, err);
+        static const char *kinds[] = {"gemm", "dw", "direct", "elt", "resize", "gap", "dwpw"};
+        static const char *acts[] = {"none", "relu", "clip", "prelu", "sigmoid"};
+        std::string t;
+        char line[512];
+        auto ref = [](const zr::TRef &r) {
+            char b[96];
+            snprintf(b, sizeof b, "%s%d[%dx%dx%d]", r.kind == 0 ? "t" : r.kind == 1 ? "in" : "out",
+                     r.id, r.C, r.H, r.W);
+            return std::string(b);
+        };
+        snprintf(line, sizeof line, "input %s %dx%dx%d arena_per_image=%lld weights=%zu bytes/img=%.0f flops/img=%.0f fusable=%d\n",
+                 plan.input_name.c_str(), plan.in_C, plan.in_H, plan.in_W,
+                 (long long)plan.arena_per_image, plan.weights.size(), plan.bytes_per_image,
+                 plan.flops_per_image, plan.input_fusable ? 1 : 0);
         t += line;
-    }
-    for (auto &st : plan.steps) {
-        snprintf(line, sizeof line,
-                 "%s%s in=%s out=%s k=%dx%d s=%d M=%d K=%d KK=%d pre=%s post=%s res=%d rC=%d elt=%d off=%lld oN=%lld oC=%lld oP=%lld\n",
-                 kinds[st.kind], st.stem ? " stem" : "", ref(st.in).c_str(), ref(st.out).c_str(), st.kh, st.kw, st.stride,
-                 st.M, st.K, st.KK, acts[st.pre.kind], acts[st.post.kind], st.res_mode, st.r_C,
-                 st.elt_op, (long long)st.out.off, (long long)st.out.o_sN, (long long)st.out.o_sC,
-                 (long long)st.out.o_sP);
-        t += line;
-    }
-    if (needed) *needed = t.size() + 1;
-    if (buf && cap) {
-        size_t n = std::min(cap - 1, t.size());
-        memcpy(buf, t.data(), n);
-        buf[n] = 0;
-    }
-    return ZR_OK;
+        for (auto &o : plan.outputs) {
+            snprintf(line, sizeof line, "output %s per_image=%lld\n", o.name.c_str(), (long long)o.per_image);
+            t += line;
+        }
+        for (auto &st : plan.steps) {
+            snprintf(line, sizeof line,
+                     "%s%s in=%s out=%s k=%dx%d s=%d M=%d K=%d KK=%d pre=%s post=%s res=%d rC=%d elt=%d off=%lld oN=%lld oC=%lld oP=%lld\n",
+                     kinds[st.kind], st.stem ? " stem" : "", ref(st.in).c_str(), ref(st.out).c_str(), st.kh, st.kw, st.stride,
+                     st.M, st.K, st.KK, acts[st.pre.kind], acts[st.post.kind], st.res_mode, st.r_C,
+                     st.elt_op, (long long)st.out.off, (long long)st.out.o_sN, (long long)st.out.o_sC,
+                     (long long)st.out.o_sP);
+            t += line;
+        }
+        if (needed) *needed = t.size() + 1;
+        if (buf && cap) {
+            size_t n = std::min(cap - 1, t.size());
+            memcpy(buf, t.data(), n);
+            buf[n] = 0;
+        }
+        return ZR_OK;
+    });
 }
 
 int zr_profile_enable(zr_session *s, int enable) {
-    if (int rc = check_session(s)) return rc;
-    std::lock_guard<std::mutex> g(s->prof.mu);
-    s->prof.on = enable != 0;
-    return ZR_OK;
+    return guarded([&]() -> int {
+        if (int rc = check_session(s)) return rc;
+        std::lock_guard<std::mutex> g(s->prof.mu);
+        s->prof.on = enable != 0;
+        return ZR_OK;
+    });
 }
 
 int zr_profile_read(zr_session *s, char *buf, size_t cap, size_t *needed) {
-    if (int rc = check_session(s)) return rc;
-    std::lock_guard<std::mutex> g(s->prof.mu);
-    struct Agg {
-        size_t n = 0;
-        double ms = 0, bytes = 0, flops = 0;
-    };
-    std::vector<std::pair<std::string, Agg>> aggs;
-    for (auto &r : s->prof.recs) {
-        HIP_TRY(hipEventSynchronize(r.b));
-        float ms = 0.f;
-        HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));
-        auto it = std::find_if(aggs.begin(), aggs.end(), [&](auto &p) { return p.first == r.kernel; });
-        if (it == aggs.end()) {
-            aggs.push_back({r.kernel, Agg{}});
-            it = aggs.end() - 1;
+    return guarded([&]() -> int {
+        if (int rc = check_session(s)) return rc;
+        std::lock_guard<std::mutex> g(s->prof.mu);
+        struct Agg {
+            size_t n = 0;
+            double ms = 0, bytes = 0, flops = 0;
+        };
+        std::vector<std::pair<std::string, Agg>> aggs;
+        for (auto &r : s->prof.recs) {
+            HIP_TRY(hipEventSynchronize(r.b));
+            float ms = 0.f;
+            HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));
+            auto it = std::find_if(aggs.begin(), aggs.end(), [&](auto &p) { return p.first == r.kernel; });
+            if (it == aggs.end()) {
+                aggs.push_back({r.kernel, Agg{}});
+                it = aggs.end() - 1;
+            }
+            it->second.n++;
+            it->second.ms += ms;
+            it->second.bytes += r.bytes;
+            it->second.flops += r.flops;
+            s->prof.pool.push_back(r.a);
+            s->prof.pool.push_back(r.b);
         }
-        it->second.n++;
-        it->second.ms += ms;
-        it->second.bytes += r.bytes;
-        it->second.flops += r.flops;
-        s->prof.pool.push_back(r.a);
-        s->prof.pool.push_back(r.b);
-    }
-    s->prof.recs.clear();
-    std::string t;
-    char line[256];
-    for (auto &a : aggs) {
-        snprintf(line, sizeof line, "%s %zu %.6f %.0f %.0f\n", a.first.c_str(), a.second.n, a.second.ms,
-                 a.second.bytes, a.second.flops);
-        t += line;
-    }
-    if (needed) *needed = t.size() + 1;
-    if (buf && cap) {
-        size_t n = std::min(cap - 1, t.size());
-        memcpy(buf, t.data(), n);
-        buf[n] = 0;
-    }
-    return ZR_OK;
+        s->prof.recs.clear();
+        std::string t;
+        char line[256];
+        for (auto &a : aggs) {
+            snprintf(line, sizeof line, "%s %zu %.6f %.0f %.0f\n", a.first.c_str(), a.second.n, a.second.ms,
+                     a.second.bytes, a.second.flops);
+            t += line;
+        }
+        if (needed) *needed = t.size() + 1;
+        if (buf && cap) {
+            size_t n = std::min(cap - 1, t.size());
+            memcpy(buf, t.data(), n);
+            buf[n] = 0;
+        }
+        return ZR_OK;
+    });
 }
 
 int zr_session_stats(const zr_session *s, double *bytes, double *flops, size_t *launches) {
-    if (int rc = check_session(s)) return rc;
-    if (bytes) *bytes = s->plan.bytes_per_image;
-    if (flops) *flops = s->plan.flops_per_image;
-    if (launches) *launches = s->plan.steps.size();
-    return ZR_OK;
+    return guarded([&]() -> int {
+        if (int rc = check_session(s)) return rc;
+        if (bytes) *bytes = s->plan.bytes_per_image;
+        if (flops) *flops = s->plan.flops_per_image;
+        if (launches) *launches = s->plan.steps.size();
+        return ZR_OK;
+    });
 }
 
 int zr_session_run_async(zr_session *s, size_t batch, const float *d_input, float *const *d_outputs,
                          size_t n_out, void *hip_stream) {
-    if (int rc = check_session(s)) return rc;
-    if (!d_input || !d_outputs || batch == 0) return set_err(ZR_ERR_INVALID_ARGUMENT, "null tensor or empty batch");
-    if (n_out != s->plan.outputs.size()) return set_err(ZR_ERR_SHAPE, "output count mismatch");
-    Ctx *c = s->acquire();
-    if (!c) return set_err(ZR_ERR_DEVICE, "cannot create execution context");
-    CtxLock lk(c);
-    HIP_TRY(hipSetDevice(s->device));
-    const int64_t hw = (int64_t)s->plan.in_H * s->plan.in_W;
-    return enqueue(s, c, (int)batch, d_input, hw * s->plan.in_C, hw, d_outputs,
-                   (hipStream_t)hip_stream);
+    return guarded([&]() -> int {
+        if (int rc = check_session(s)) return rc;
+        if (!d_input || !d_outputs || batch == 0) return set_err(ZR_ERR_INVALID_ARGUMENT, "null tensor or empty batch");
+        if (n_out != s->plan.outputs.size()) return set_err(ZR_ERR_SHAPE, "output count mismatch");
+        Ctx *c = s->acquire();
+        if (!c) return set_err(ZR_ERR_DEVICE, "cannot create execution context");
+        CtxLock lk(c);
+        HIP_TRY(hipSetDevice(s->device));
+        const int64_t hw = (int64_t)s->plan.in_H * s->plan.in_W;
+        return enqueue(s, c, (int)batch, d_input, hw * s->plan.in_C, hw, d_outputs,
+                       (hipStream_t)hip_stream);
+    });
 }
 
 int zr_session_run(zr_session *s, size_t batch, const float *const *inputs, size_t n_in,
                    float *const *outputs, size_t n_out) {
-    if (int rc = check_session(s)) return rc;
-    if (!inputs || !outputs || batch == 0) return set_err(ZR_ERR_INVALID_ARGUMENT, "null tensor or empty batch");
-    if (n_in != 1) return set_err(ZR_ERR_SHAPE, "CNN sessions take exactly 1 input");
-    if (n_out != s->plan.outputs.size()) return set_err(ZR_ERR_SHAPE, "output count mismatch");
-    Ctx *c = s->acquire();
-    if (!c) return set_err(ZR_ERR_DEVICE, "cannot create execution context");
-    CtxLock lk(c);
-    HIP_TRY(hipSetDevice(s->device));
-    const int64_t hw = (int64_t)s->plan.in_H * s->plan.in_W;
-    const size_t in_floats = (size_t)hw * s->plan.in_C * batch;
-    if (int rc = grow(c->input, c->input_floats, in_floats)) return rc;
-    if (int rc = sync_outputs(s, c, batch)) return rc;
-    HIP_TRY(hipMemcpyAsync(c->input, inputs[0], in_floats * 4, hipMemcpyHostToDevice, c->stream));
-    if (int rc = enqueue(s, c, (int)batch, c->input, hw * s->plan.in_C, hw, c->outs.data(), c->stream))
-        return rc;
-    for (size_t i = 0; i < n_out; i++)
-        HIP_TRY(hipMemcpyAsync(outputs[i], c->outs[i], s->plan.outputs[i].per_image * batch * 4,
-                               hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return ZR_OK;
+    return guarded([&]() -> int {
+        if (int rc = check_session(s)) return rc;
+        if (!inputs || !outputs || batch == 0) return set_err(ZR_ERR_INVALID_ARGUMENT, "null tensor or empty batch");
+        if (n_in != 1) return set_err(ZR_ERR_SHAPE, "CNN sessions take exactly 1 input");
+        if (n_out != s->plan.outputs.size()) return set_err(ZR_ERR_SHAPE, "output count mismatch");
+        Ctx *c = s->acquire();
+        if (!c) return set_err(ZR_ERR_DEVICE, "cannot create execution context");
+        CtxLock lk(c);
+        HIP_TRY(hipSetDevice(s->device));
+        const int64_t hw = (int64_t)s->plan.in_H * s->plan.in_W;
+        const size_t in_floats = (size_t)hw * s->plan.in_C * batch;
+        if (int rc = grow(c->input, c->input_floats, in_floats)) return rc;
+        if (int rc = sync_outputs(s, c, batch)) return rc;
+        HIP_TRY(hipMemcpyAsync(c->input, inputs[0], in_floats * 4, hipMemcpyHostToDevice, c->stream));
+        if (int rc = enqueue(s, c, (int)batch, c->input, hw * s->plan.in_C, hw, c->outs.data(), c->stream))
+            return rc;
+        for (size_t i = 0; i < n_out; i++)
+            HIP_TRY(hipMemcpyAsync(outputs[i], c->outs[i], s->plan.outputs[i].per_image * batch * 4,
+                                   hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return ZR_OK;
+    });
 }
 
 static int views_common(zr_session *s, Ctx *c, const zr_frame *frames, size_t nf, const zr_view *views,
@@ -499,12 +539,13 @@ static int views_common(zr_session *s, Ctx *c, const zr_frame *frames, size_t nf
     p.o_sN = hw;                    // CNHW straight into the plan's input layout
     p.o_sC = hw * (int64_t)nv;
     {
+        const bool prof = s->prof.on.load();
         std::unique_lock<std::mutex> pl(s->prof.mu, std::defer_lock);
-        if (s->prof.on) pl.lock();
-        if (s->prof.on) s->prof.before(stream);
+        if (prof) pl.lock();
+        if (prof) s->prof.before(stream);
         const char *k = zr::launch_preproc(p, stream);
         // algorithmic bytes: RGBA gather 4 B + 3 f32 writes per output position
-        if (s->prof.on) s->prof.after(stream, k, 16.0 * (double)hw * nv, 0.0);
+        if (prof) s->prof.after(stream, k, 16.0 * (double)hw * nv, 0.0);
     }
     HIP_TRY(hipGetLastError());
     return enqueue(s, c, (int)nv, c->input, hw, hw * (int64_t)nv, outs, stream);
@@ -513,184 +554,220 @@ static int views_common(zr_session *s, Ctx *c, const zr_frame *frames, size_t nf
 int zr_cnn_estimate_views_async(zr_session *s, const zr_frame *frames, size_t n_frames,
                                 const zr_view *views, const uint32_t *view_frame, size_t n_views,
                                 float lo, float hi, float *const *d_outputs, void *hip_stream) {
-    if (int rc = check_session(s)) return rc;
-    if (!frames || !views || !d_outputs || n_views == 0)
-        return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument or no views");
-    Ctx *c = s->acquire();
-    if (!c) return set_err(ZR_ERR_DEVICE, "cannot create execution context");
-    CtxLock lk(c);
-    HIP_TRY(hipSetDevice(s->device));
-    return views_common(s, c, frames, n_frames, views, view_frame, n_views, lo, hi, d_outputs,
-                        (hipStream_t)hip_stream);
+    return guarded([&]() -> int {
+        if (int rc = check_session(s)) return rc;
+        if (!frames || !views || !d_outputs || n_views == 0)
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument or no views");
+        Ctx *c = s->acquire();
+        if (!c) return set_err(ZR_ERR_DEVICE, "cannot create execution context");
+        CtxLock lk(c);
+        HIP_TRY(hipSetDevice(s->device));
+        return views_common(s, c, frames, n_frames, views, view_frame, n_views, lo, hi, d_outputs,
+                            (hipStream_t)hip_stream);
+    });
 }
 
 int zr_cnn_estimate_views(zr_session *s, const uint8_t *rgba, uint32_t w, uint32_t h,
                           size_t row_stride, const zr_view *views, size_t n_views, float lo,
                           float hi, float *const *outputs) {
-    if (int rc = check_session(s)) return rc;
-    if (!rgba || !views || !outputs || n_views == 0)
-        return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument or no views");
-    if (row_stride < (size_t)w * 4) return set_err(ZR_ERR_INVALID_ARGUMENT, "row_stride < 4*width");
-    Ctx *c = s->acquire();
-    if (!c) return set_err(ZR_ERR_DEVICE, "cannot create execution context");
-    CtxLock lk(c);
-    HIP_TRY(hipSetDevice(s->device));
-    const size_t bytes = row_stride * h;
-    if (int rc = grow(c->image, c->image_bytes, bytes ? bytes : 4)) return rc;
-    if (int rc = sync_outputs(s, c, n_views)) return rc;
-    HIP_TRY(hipStreamWaitEvent(c->stream, c->done, 0));
-    HIP_TRY(hipMemcpyAsync(c->image, rgba, bytes, hipMemcpyHostToDevice, c->stream));
-    zr_frame f{c->image, w, h, (uint64_t)row_stride};
-    if (int rc = views_common(s, c, &f, 1, views, nullptr, n_views, lo, hi, c->outs.data(), c->stream))
-        return rc;
-    for (size_t i = 0; i < s->plan.outputs.size(); i++)
-        HIP_TRY(hipMemcpyAsync(outputs[i], c->outs[i], s->plan.outputs[i].per_image * n_views * 4,
-                               hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return ZR_OK;
+    return guarded([&]() -> int {
+        if (int rc = check_session(s)) return rc;
+        if (!rgba || !views || !outputs || n_views == 0)
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument or no views");
+        if (row_stride < (size_t)w * 4) return set_err(ZR_ERR_INVALID_ARGUMENT, "row_stride < 4*width");
+        Ctx *c = s->acquire();
+        if (!c) return set_err(ZR_ERR_DEVICE, "cannot create execution context");
+        CtxLock lk(c);
+        HIP_TRY(hipSetDevice(s->device));
+        const size_t bytes = row_stride * h;
+        if (int rc = grow(c->image, c->image_bytes, bytes ? bytes : 4)) return rc;
+        if (int rc = sync_outputs(s, c, n_views)) return rc;
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->done, 0));
+        HIP_TRY(hipMemcpyAsync(c->image, rgba, bytes, hipMemcpyHostToDevice, c->stream));
+        zr_frame f{c->image, w, h, (uint64_t)row_stride};
+        if (int rc = views_common(s, c, &f, 1, views, nullptr, n_views, lo, hi, c->outs.data(), c->stream))
+            return rc;
+        for (size_t i = 0; i < s->plan.outputs.size(); i++)
+            HIP_TRY(hipMemcpyAsync(outputs[i], c->outs[i], s->plan.outputs[i].per_image * n_views * 4,
+                                   hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return ZR_OK;
+    });
 }
 
 int zr_preprocess_views_async(const zr_frame *frames, size_t n_frames, const zr_view *views,
                               const uint32_t *view_frame, size_t n_views, uint32_t ow, uint32_t oh,
                               float lo, float hi, float *d_out, void *hip_stream) {
-    if (!frames || !views || !d_out || n_views == 0 || ow == 0 || oh == 0)
-        return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument or empty shape");
-    if (!(hi > lo)) return set_err(ZR_ERR_INVALID_ARGUMENT, "ColorMapper range must satisfy end > start");
-    hipStream_t st = (hipStream_t)hip_stream;
-    std::vector<zr::ViewDesc> vd(n_views);
-    for (size_t i = 0; i < n_views; i++) {
-        const uint32_t f = view_frame ? view_frame[i] : 0;
-        if (f >= n_frames) return set_err(ZR_ERR_INVALID_ARGUMENT, "view_frame index out of range");
-        vd[i] = make_view(views[i], f);
-    }
-    std::vector<zr::FrameDesc> fd(n_frames);
-    for (size_t i = 0; i < n_frames; i++)
-        if (!frames[i].rgba || frames[i].width == 0 || frames[i].height == 0)
-            return set_err(ZR_ERR_INVALID_ARGUMENT, "empty frame");
-    for (size_t i = 0; i < n_frames; i++)
-        fd[i] = zr::FrameDesc{frames[i].rgba, frames[i].width, frames[i].height, frames[i].row_stride};
-    zr::ViewDesc *dv = nullptr;
-    zr::FrameDesc *df = nullptr;
-    HIP_TRY(hipMallocAsync((void **)&dv, n_views * sizeof(zr::ViewDesc), st));
-    HIP_TRY(hipMallocAsync((void **)&df, n_frames * sizeof(zr::FrameDesc), st));
-    HIP_TRY(hipMemcpyAsync(dv, vd.data(), n_views * sizeof(zr::ViewDesc), hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(df, fd.data(), n_frames * sizeof(zr::FrameDesc), hipMemcpyHostToDevice, st));
-    zr::PreprocParams p{};
-    p.frames = df;
-    p.views = dv;
-    p.nviews = (int)n_views;
-    p.OW = (int)ow;
-    p.OH = (int)oh;
-    p.lo = lo;
-    p.adjust = (hi - lo) / 255.0f;
-    p.out = d_out;
-    p.o_sN = 3 * (int64_t)ow * oh;
-    p.o_sC = (int64_t)ow * oh;
-    zr::launch_preproc(p, st);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipFreeAsync(dv, st));
-    HIP_TRY(hipFreeAsync(df, st));
-    return ZR_OK;
+    return guarded([&]() -> int {
+        if (!frames || !views || !d_out || n_views == 0 || ow == 0 || oh == 0)
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument or empty shape");
+        if (!(hi > lo)) return set_err(ZR_ERR_INVALID_ARGUMENT, "ColorMapper range must satisfy end > start");
+        hipStream_t st = (hipStream_t)hip_stream;
+        std::vector<zr::ViewDesc> vd(n_views);
+        for (size_t i = 0; i < n_views; i++) {
+            const uint32_t f = view_frame ? view_frame[i] : 0;
+            if (f >= n_frames) return set_err(ZR_ERR_INVALID_ARGUMENT, "view_frame index out of range");
+            vd[i] = make_view(views[i], f);
+        }
+        std::vector<zr::FrameDesc> fd(n_frames);
+        for (size_t i = 0; i < n_frames; i++)
+            if (!frames[i].rgba || frames[i].width == 0 || frames[i].height == 0)
+                return set_err(ZR_ERR_INVALID_ARGUMENT, "empty frame");
+        for (size_t i = 0; i < n_frames; i++)
+            fd[i] = zr::FrameDesc{frames[i].rgba, frames[i].width, frames[i].height, frames[i].row_stride};
+        zr::ViewDesc *dv = nullptr;
+        zr::FrameDesc *df = nullptr;
+        HIP_TRY(hipMallocAsync((void **)&dv, n_views * sizeof(zr::ViewDesc), st));
+        HIP_TRY(hipMallocAsync((void **)&df, n_frames * sizeof(zr::FrameDesc), st));
+        HIP_TRY(hipMemcpyAsync(dv, vd.data(), n_views * sizeof(zr::ViewDesc), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(df, fd.data(), n_frames * sizeof(zr::FrameDesc), hipMemcpyHostToDevice, st));
+        zr::PreprocParams p{};
+        p.frames = df;
+        p.views = dv;
+        p.nviews = (int)n_views;
+        p.OW = (int)ow;
+        p.OH = (int)oh;
+        p.lo = lo;
+        p.adjust = (hi - lo) / 255.0f;
+        p.out = d_out;
+        p.o_sN = 3 * (int64_t)ow * oh;
+        p.o_sC = (int64_t)ow * oh;
+        zr::launch_preproc(p, st);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipFreeAsync(dv, st));
+        HIP_TRY(hipFreeAsync(df, st));
+        return ZR_OK;
+    });
 }
 
 int zr_detection_candidates_async(const float *d_logits, const float *d_boxes, uint32_t n,
                                   uint32_t anchors, uint32_t params, float logit_min,
                                   uint32_t cap, int32_t *d_count, float *d_rec, void *hip_stream) {
-    if (!d_logits || !d_boxes || !d_count || !d_rec) return set_err(ZR_ERR_INVALID_ARGUMENT, "null pointer");
-    if (n == 0) return ZR_OK;
-    zr::CandParams p{};
-    p.logits = d_logits;
-    p.boxes = d_boxes;
-    p.N = (int)n;
-    p.A = (int)anchors;
-    p.D = (int)params;
-    p.cap = (int)cap;
-    p.logit_min = logit_min;
-    p.count = d_count;
-    p.rec = d_rec;
-    zr::launch_candidates(p, (hipStream_t)hip_stream);
-    HIP_TRY(hipGetLastError());
-    return ZR_OK;
+    return guarded([&]() -> int {
+        if (!d_logits || !d_boxes || !d_count || !d_rec) return set_err(ZR_ERR_INVALID_ARGUMENT, "null pointer");
+        if (n == 0) return ZR_OK;
+        zr::CandParams p{};
+        p.logits = d_logits;
+        p.boxes = d_boxes;
+        p.N = (int)n;
+        p.A = (int)anchors;
+        p.D = (int)params;
+        p.cap = (int)cap;
+        p.logit_min = logit_min;
+        p.count = d_count;
+        p.rec = d_rec;
+        zr::launch_candidates(p, (hipStream_t)hip_stream);
+        HIP_TRY(hipGetLastError());
+        return ZR_OK;
+    });
 }
 
 int zr_device_count(int *n) {
-    if (!n) return set_err(ZR_ERR_INVALID_ARGUMENT, "null n");
-    *n = 0;
-    if (hipGetDeviceCount(n) != hipSuccess) *n = 0;
-    return ZR_OK;
+    return guarded([&]() -> int {
+        if (!n) return set_err(ZR_ERR_INVALID_ARGUMENT, "null n");
+        *n = 0;
+        if (hipGetDeviceCount(n) != hipSuccess) *n = 0;
+        return ZR_OK;
+    });
 }
 
 int zr_malloc(void **p, size_t bytes) {
-    if (!p) return set_err(ZR_ERR_INVALID_ARGUMENT, "null p");
-    HIP_TRY(hipMalloc(p, bytes ? bytes : 4));
-    return ZR_OK;
+    return guarded([&]() -> int {
+        if (!p) return set_err(ZR_ERR_INVALID_ARGUMENT, "null p");
+        HIP_TRY(hipMalloc(p, bytes ? bytes : 4));
+        return ZR_OK;
+    });
 }
 
 int zr_free(void *p) {
-    HIP_TRY(hipFree(p));
-    return ZR_OK;
+    return guarded([&]() -> int {
+        HIP_TRY(hipFree(p));
+        return ZR_OK;
+    });
 }
 
 int zr_host_alloc(void **p, size_t bytes) {
-    if (!p) return set_err(ZR_ERR_INVALID_ARGUMENT, "null p");
-    HIP_TRY(hipHostMalloc(p, bytes ? bytes : 4));
-    return ZR_OK;
+    return guarded([&]() -> int {
+        if (!p) return set_err(ZR_ERR_INVALID_ARGUMENT, "null p");
+        HIP_TRY(hipHostMalloc(p, bytes ? bytes : 4));
+        return ZR_OK;
+    });
 }
 
 int zr_host_free(void *p) {
-    HIP_TRY(hipHostFree(p));
-    return ZR_OK;
+    return guarded([&]() -> int {
+        HIP_TRY(hipHostFree(p));
+        return ZR_OK;
+    });
 }
 
 int zr_memcpy_async(void *dst, const void *src, size_t bytes, int kind, void *hip_stream) {
-    hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost
-                                                                    : hipMemcpyDeviceToDevice;
-    HIP_TRY(hipMemcpyAsync(dst, src, bytes, k, (hipStream_t)hip_stream));
-    return ZR_OK;
+    return guarded([&]() -> int {
+        hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost
+                                                                        : hipMemcpyDeviceToDevice;
+        HIP_TRY(hipMemcpyAsync(dst, src, bytes, k, (hipStream_t)hip_stream));
+        return ZR_OK;
+    });
 }
 
 int zr_event_create(void **event) {
-    if (!event) return set_err(ZR_ERR_INVALID_ARGUMENT, "null event");
-    HIP_TRY(hipEventCreateWithFlags((hipEvent_t *)event, hipEventDisableTiming));
-    return ZR_OK;
+    return guarded([&]() -> int {
+        if (!event) return set_err(ZR_ERR_INVALID_ARGUMENT, "null event");
+        HIP_TRY(hipEventCreateWithFlags((hipEvent_t *)event, hipEventDisableTiming));
+        return ZR_OK;
+    });
 }
 
 int zr_event_destroy(void *event) {
-    HIP_TRY(hipEventDestroy((hipEvent_t)event));
-    return ZR_OK;
+    return guarded([&]() -> int {
+        HIP_TRY(hipEventDestroy((hipEvent_t)event));
+        return ZR_OK;
+    });
 }
 
 int zr_event_record(void *event, void *stream) {
-    HIP_TRY(hipEventRecord((hipEvent_t)event, (hipStream_t)stream));
-    return ZR_OK;
+    return guarded([&]() -> int {
+        HIP_TRY(hipEventRecord((hipEvent_t)event, (hipStream_t)stream));
+        return ZR_OK;
+    });
 }
 
 int zr_event_synchronize(void *event) {
-    HIP_TRY(hipEventSynchronize((hipEvent_t)event));
-    return ZR_OK;
+    return guarded([&]() -> int {
+        HIP_TRY(hipEventSynchronize((hipEvent_t)event));
+        return ZR_OK;
+    });
 }
 
 int zr_event_query(void *event) {
-    const hipError_t e = hipEventQuery((hipEvent_t)event);
-    if (e == hipSuccess) return ZR_OK;
-    if (e == hipErrorNotReady) return 1;
-    return set_err(ZR_ERR_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
+    return guarded([&]() -> int {
+        const hipError_t e = hipEventQuery((hipEvent_t)event);
+        if (e == hipSuccess) return ZR_OK;
+        if (e == hipErrorNotReady) return 1;
+        return set_err(ZR_ERR_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
+    });
 }
 
 int zr_stream_create(void **stream) {
-    if (!stream) return set_err(ZR_ERR_INVALID_ARGUMENT, "null stream");
-    HIP_TRY(hipStreamCreateWithFlags((hipStream_t *)stream, hipStreamNonBlocking));
-    return ZR_OK;
+    return guarded([&]() -> int {
+        if (!stream) return set_err(ZR_ERR_INVALID_ARGUMENT, "null stream");
+        HIP_TRY(hipStreamCreateWithFlags((hipStream_t *)stream, hipStreamNonBlocking));
+        return ZR_OK;
+    });
 }
 
 int zr_stream_destroy(void *stream) {
-    HIP_TRY(hipStreamDestroy((hipStream_t)stream));
-    return ZR_OK;
+    return guarded([&]() -> int {
+        HIP_TRY(hipStreamDestroy((hipStream_t)stream));
+        return ZR_OK;
+    });
 }
 
 int zr_stream_synchronize(void *stream) {
-    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-    return ZR_OK;
+    return guarded([&]() -> int {
+        HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+        return ZR_OK;
+    });
 }
 
 }  // extern "C"

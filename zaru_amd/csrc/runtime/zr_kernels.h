@@ -176,6 +176,11 @@ bool stem_supported(int cin, int k, int stride, int cout);
 bool dwpw_supported(int k, int stride);
 
 // launchers (kernels/*.hip); each returns the symbol of the kernel it launched
+// The symbol a launch ran, as rocprofv3 prints it (spaces removed), for the profiler: printf
+// formatting interned in a mutex-guarded set, so the pointer stays valid and concurrent
+// launches from several threads are safe.
+const char *kernel_name(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+
 const char *launch_gemm(const GemmParams &p, hipStream_t s);
 const char *launch_dw(const DwParams &p, hipStream_t s);
 const char *launch_direct(const DirectParams &p, hipStream_t s);
