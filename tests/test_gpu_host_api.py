@@ -134,9 +134,18 @@ def test_repeated_runs_equal_single_run(H):
     n1 = p.run_frames()
     want = [(r["frame"], r["landmarks"].copy(), r["tracked"]) for r in (p.roi(i) for i in range(n1))]
     want_det = [[(d.confidence(), d.bounding_rect().tuple()) for d in ds] for ds in p.detections()]
-    total = p.run_frames_repeated(3)
-    assert total == 3 * n1 and p.num_rois() == n1
-    for i, (f, lm, tr) in enumerate(want):
-        r = p.roi(i)
-        assert r["frame"] == f and r["tracked"] == tr and np.array_equal(r["landmarks"], lm)
-    assert [[(d.confidence(), d.bounding_rect().tuple()) for d in ds] for ds in p.detections()] == want_det
+    tracked = p.run_frames_repeated(3)
+    assert p.times()["rois"] == 3 * n1 and p.num_rois() == n1
+    assert tracked == 3 * sum(tr for _, _, tr in want)
+
+    def same():
+        for i, (f, lm, tr) in enumerate(want):
+            r = p.roi(i)
+            assert r["frame"] == f and r["tracked"] == tr and np.array_equal(r["landmarks"], lm)
+        assert [[(d.confidence(), d.bounding_rect().tuple()) for d in ds] for ds in p.detections()] == want_det
+    same()
+    # the step-at-a-time form (multi-GPU bench: all-gather between steps): every step's results
+    p.begin_steps()
+    for k in range(3):
+        p.step(k < 2)
+        same()

@@ -87,3 +87,63 @@ def test_all_gather_world2_gloo():
         assert sorted(got) == list(range(n_frames))
         for f in range(n_frames):
             assert got[f] == want[f]
+
+
+def _gather_worker(rank, world, port, steps, q):
+    """A stand-in pipeline: step k yields frame records whose ids encode (step, rank); the
+    gather of every step must hold every rank's records, while the loop never waits for it."""
+    import time
+
+    import torch.distributed as dist
+    import zaru_amd.host as H
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        B = 6
+        g = shard.RecordGather(B, shard.record_width(), "cpu")
+        got = []
+        t0 = time.perf_counter()
+        for k in range(steps):
+            mine = shard.frames_of_rank(B * world, rank, world)
+            recs = H.pack_detection_records([_frame_detections(H, f) for f in mine],
+                                            [1000 * k + f for f in mine], 8)
+            time.sleep(0.01)  # the pipeline step
+            g.submit(recs)
+            if k >= 1:  # the previous step's gather has had a whole step to finish
+                got.append(g.result(k - 1).numpy().copy())
+        g.finish()
+        got.append(g.result(steps - 1).numpy().copy())
+        q.put((rank, got, time.perf_counter() - t0))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_record_gather_overlaps_steps_world2_gloo():
+    world, steps = 2, 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    for _ in range(world):
+        r, got, dt = q.get(timeout=180)
+        results[r] = (got, dt)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import zaru_amd.host as H
+    for rank in range(world):
+        got, dt = results[rank]
+        assert len(got) == steps
+        for k in range(steps):
+            assert np.array_equal(got[k], results[0][0][k])
+            recs = shard.unpack_records(got[k])
+            assert sorted(recs) == [1000 * k + f for f in range(6 * world)]
+            for f in range(6 * world):
+                want = [tuple(float(np.float32(v)) for v in
+                              (d.confidence(), d.angle(), *d.bounding_rect().tuple(),
+                               *[c for kp in d.keypoints() for c in kp]))
+                        for d in _frame_detections(H, f)][:8]
+                assert recs[1000 * k + f] == want

@@ -336,8 +336,17 @@ PYBIND11_MODULE(_zaru_host, m) {
         .def("run_frames_repeated", [](DetectTrackPipeline &p, int steps) {
             py::gil_scoped_release nogil;
             p.run_frames_repeated(steps);
-            return p.times().rois;
+            return p.times().tracked;
         }, py::arg("steps"))
+        .def("begin_steps", [](DetectTrackPipeline &p) {
+            py::gil_scoped_release nogil;
+            p.begin_steps();
+        })
+        .def("step", [](DetectTrackPipeline &p, bool more) {
+            py::gil_scoped_release nogil;
+            p.step(more);
+            return p.times().tracked;
+        }, py::arg("more"))
         .def("detections", [](const DetectTrackPipeline &p) { return p.detections(); })
         .def("detection_records", [](const DetectTrackPipeline &p, uint32_t rmax, uint32_t first_id,
                                      uint32_t id_stride) {

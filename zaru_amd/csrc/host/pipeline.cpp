@@ -372,51 +372,63 @@ void DetectTrackPipeline::run(const std::vector<Image> &frames,
     times_.total_ms = ms_since(t0);
 }
 
-void DetectTrackPipeline::run_frames_repeated(int steps) {
-    const auto t0 = clk::now();
+void DetectTrackPipeline::begin_steps() {
+    steps_t0_ = clk::now();
+    times_ = StageTimes{};
     const std::vector<Image> &frames = frames_;
     const size_t B = frames.size();
-    times_ = StageTimes{};
-    if (B == 0 || steps <= 0) return;
-    const size_t S = std::min<size_t>(slots_.size(), B);
+    active_slots_ = std::min<size_t>(slots_.size(), B);
     size_t f0 = 0;
-    for (size_t k = 0; k < S; k++) {
+    for (size_t k = 0; k < active_slots_; k++) {
         Slot &s = *slots_[k];
         s.f0 = f0;
-        s.nf = B / S + (k < B % S ? 1 : 0);
+        s.nf = B / active_slots_ + (k < B % active_slots_ ? 1 : 0);
         f0 += s.nf;
         stage_detect(s, frames);
     }
-    for (int it = 0; it < steps; it++) {
-        dets_.assign(B, {});
-        rois_.clear();
-        for (size_t k = 0; k < S; k++) {
-            Slot &s = *slots_[k];
-            const auto t = clk::now();
-            check(zr_event_synchronize(s.ev_det));
-            times_.detect_gpu_ms += ms_since(t);
-            const auto t1 = clk::now();
-            stage_decode_and_rois(s, frames, forced_);
-            times_.decode_nms_ms += ms_since(t1);
-        }
-        // the next run's detections queue behind this run's landmarks on each slot's stream
-        if (it + 1 < steps)
-            for (size_t k = 0; k < S; k++) stage_detect(*slots_[k], frames);
-        for (size_t k = 0; k < S; k++) {
-            Slot &s = *slots_[k];
-            const auto t = clk::now();
-            if (s.nroi) check(zr_event_synchronize(s.ev_lm));
-            times_.landmark_gpu_ms += ms_since(t);
-            const auto t1 = clk::now();
-            stage_map(s);
-            times_.map_ms += ms_since(t1);
-        }
-        times_.frames += B;
-        times_.rois += rois_.size();
-        for (auto &d : dets_) times_.detections += d.size();
-        for (auto &r : rois_) times_.tracked += r.tracked ? 1 : 0;
+}
+
+void DetectTrackPipeline::step(bool more) {
+    const std::vector<Image> &frames = frames_;
+    const size_t B = frames.size(), S = active_slots_;
+    if (S == 0) return;
+    dets_.assign(B, {});
+    rois_.clear();
+    for (size_t k = 0; k < S; k++) {
+        Slot &s = *slots_[k];
+        const auto t = clk::now();
+        check(zr_event_synchronize(s.ev_det));
+        times_.detect_gpu_ms += ms_since(t);
+        const auto t1 = clk::now();
+        stage_decode_and_rois(s, frames, forced_);
+        times_.decode_nms_ms += ms_since(t1);
     }
-    times_.total_ms = ms_since(t0);
+    // the next run's detections queue behind this run's landmarks on each slot's stream
+    if (more)
+        for (size_t k = 0; k < S; k++) stage_detect(*slots_[k], frames);
+    for (size_t k = 0; k < S; k++) {
+        Slot &s = *slots_[k];
+        const auto t = clk::now();
+        if (s.nroi) check(zr_event_synchronize(s.ev_lm));
+        times_.landmark_gpu_ms += ms_since(t);
+        const auto t1 = clk::now();
+        stage_map(s);
+        times_.map_ms += ms_since(t1);
+    }
+    times_.frames += B;
+    times_.rois += rois_.size();
+    for (auto &d : dets_) times_.detections += d.size();
+    for (auto &r : rois_) times_.tracked += r.tracked ? 1 : 0;
+    times_.total_ms = ms_since(steps_t0_);
+}
+
+void DetectTrackPipeline::run_frames_repeated(int steps) {
+    if (frames_.empty() || steps <= 0) {
+        times_ = StageTimes{};
+        return;
+    }
+    begin_steps();
+    for (int it = 0; it < steps; it++) step(it + 1 < steps);
 }
 
 }  // namespace zh

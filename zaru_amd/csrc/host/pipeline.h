@@ -105,6 +105,13 @@ class DetectTrackPipeline {
     // before this run's landmark mapping, so the GPU never waits for the host between runs.
     // Results are the last run's; times() sums all runs.
     void run_frames_repeated(int steps);
+    // The same, one step at a time, so a caller can act between steps (the multi-GPU
+    // all-gather of each step's detections): begin_steps() enqueues the first detections,
+    // each step(more) finishes one run over the resident frames -- with more = true the next
+    // run's detections are enqueued before this run's landmark mapping -- and leaves its
+    // results readable until the next step.  Every begun sequence ends with step(false).
+    void begin_steps();
+    void step(bool more);
 
   private:
     // one software-pipeline slot: a contiguous range of frames with its own stream/buffers
@@ -139,6 +146,8 @@ class DetectTrackPipeline {
     StageTimes times_;
     std::vector<Image> frames_;
     std::vector<std::vector<RotatedRect>> forced_;
+    size_t active_slots_ = 0;
+    std::chrono::steady_clock::time_point steps_t0_;
 };
 
 }  // namespace zh

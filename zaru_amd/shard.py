@@ -57,3 +57,75 @@ def all_gather_records(local, group=None):
     else:
         dist.all_gather(list(out.chunk(world)), local.contiguous(), group=group)
     return out
+
+
+class RecordGather:
+    """The per-step all-gather of detection records, overlapped with the next steps.
+
+    ``submit(recs)`` takes one step's host records ([B, W] f32, ``DetectTrackPipeline.
+    detection_records``), stages them in a pinned buffer, copies them to the device and starts
+    the all-gather asynchronously (``async_op=True``: RCCL runs it on its own stream, gloo on its
+    own thread), then returns at once, so the pipeline's next step starts while the collective is
+    in flight.  Two slots alternate; a slot is reused only after its previous copy and gather
+    completed.  ``finish()`` waits for the collectives still in flight; ``result(step)`` is the
+    [world * B, W] gathered tensor of a finished step (rank-major, frames of rank r first).
+    One collective per step and no other: SURVEY.md §8e.
+    """
+
+    def __init__(self, rows: int, width: int, device, group=None):
+        import torch
+        import torch.distributed as dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.nccl = dist.get_backend(group) == "nccl"
+        self.device = torch.device(device)
+        cuda = self.device.type == "cuda"
+        self.host = [torch.empty((rows, width), dtype=torch.float32, pin_memory=cuda) for _ in range(2)]
+        self.inp = [torch.empty((rows, width), dtype=torch.float32, device=self.device) for _ in range(2)]
+        self.out = [torch.empty((self.world * rows, width), dtype=torch.float32, device=self.device)
+                    for _ in range(2)]
+        self.copied = [torch.cuda.Event() if cuda else None for _ in range(2)]
+        self.work = [None, None]
+        self.step_of = [-1, -1]
+        self.steps = 0
+
+    def _wait(self, k):
+        if self.work[k] is not None:
+            self.work[k].wait()
+            self.work[k] = None
+        if self.copied[k] is not None:
+            self.copied[k].synchronize()  # the pinned slot may be rewritten
+
+    def submit(self, recs: np.ndarray) -> None:
+        import torch
+        import torch.distributed as dist
+        k = self.steps & 1
+        self._wait(k)
+        self.host[k].numpy()[...] = recs
+        if self.device.type == "cuda":
+            self.inp[k].copy_(self.host[k], non_blocking=True)
+            self.copied[k].record()
+        else:
+            self.inp[k].copy_(self.host[k])
+        if self.nccl:
+            self.work[k] = dist.all_gather_into_tensor(self.out[k], self.inp[k], group=self.group,
+                                                       async_op=True)
+        else:
+            self.work[k] = dist.all_gather(list(self.out[k].chunk(self.world)), self.inp[k],
+                                           group=self.group, async_op=True)
+        self.step_of[k] = self.steps
+        self.steps += 1
+
+    def finish(self) -> None:
+        for k in range(2):
+            self._wait(k)
+        if self.device.type == "cuda":
+            import torch
+            torch.cuda.current_stream(self.device).synchronize()
+
+    def result(self, step: int):
+        for k in range(2):
+            if self.step_of[k] == step:
+                self._wait(k)
+                return self.out[k]
+        raise KeyError(f"step {step} is no longer held (only the last two are)")
