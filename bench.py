@@ -288,13 +288,16 @@ def cpu_baseline(kind, seconds, batch, seed):
 class Workload:
     """One DetectTrackPipeline over its resident synthetic frames."""
 
-    def __init__(self, H, kind, device, batch, rank, threads, sub_batches, multi_stream):
+    def __init__(self, H, kind, device, batch, rank, threads, sub_batches, multi_stream, shared=None):
         det, lm, din, lin, rois, seed = WORKLOADS[kind]
         self.kind, self.batch, self.det, self.lm = kind, batch, det, lm
         rng = np.random.default_rng(seed + 1000 * rank)
-        self.fs = FrameSet(rng, batch, patch=load_patch() if kind == "face" else None)
+        if shared is None:
+            self.fs = FrameSet(rng, batch, patch=load_patch() if kind == "face" else None)
+            self.frames = self.fs.to_device(f"cuda:{device}")
+        else:  # config 5: the other pipeline's frames (the same camera streams)
+            self.fs, self.frames = shared.fs, shared.frames
         forced = forced_rois(rng, batch, kind)
-        self.frames = self.fs.to_device(f"cuda:{device}")
         fp, fb = self.frames.data_ptr(), 1080 * 1920 * 4
         self.flist = [(fp + i * fb, 1920, 1080, 1920 * 4) for i in range(batch)]
         self.forced = forced
@@ -367,8 +370,10 @@ def main():
 
     kinds = ["face", "hand"] if args.workload == "both" else [primary]
     threads = args.threads if len(kinds) == 1 else max(2, args.threads // 2)
-    wls = [Workload(H, k, device, args.batch, rank, threads, args.sub_batches, args.streams == "multi")
-           for k in kinds]
+    wls = []
+    for k in kinds:  # config 5: the hand pipeline runs on the face pipeline's frames
+        wls.append(Workload(H, k, device, args.batch, rank, threads, args.sub_batches,
+                            args.streams == "multi", shared=wls[0] if wls else None))
     gather = (shard.RecordGather(args.batch * len(wls), shard.record_width(), f"cuda:{device}")
               if world > 1 else None)
     pool = None

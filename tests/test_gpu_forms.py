@@ -38,6 +38,7 @@ SWITCHES = {
     "no_v4": {"ZR_DWPW_V4": "0", "ZR_DWPW_DMA": "0"},
     "no_rows": {"ZR_GEMM_ROWS": "0"},
     "dma_chunk32": {"ZR_DWPW_FKC": "32"},  # not an off-switch: the other DMA chunk size
+    "no_chain": {"ZARU_HIP_FUSE": "0"},    # the layer-per-launch plan (no chain.hip)
 }
 
 
@@ -48,7 +49,7 @@ def outputs(tmp_path_factory):
     for name, env in SWITCHES.items():
         path = str(d / f"{name}.npz")
         e = dict(os.environ)
-        for k in ("ZR_VALU_DB", "ZR_DWPW_DMA", "ZR_DWPW_V4", "ZR_GEMM_ROWS", "ZR_DWPW_FKC"):
+        for k in ("ZR_VALU_DB", "ZR_DWPW_DMA", "ZR_DWPW_V4", "ZR_GEMM_ROWS", "ZR_DWPW_FKC", "ZARU_HIP_FUSE"):
             e.pop(k, None)
         e.update(env)
         subprocess.run([sys.executable, "-c", CHILD, REPO, path], env=e, check=True, timeout=110)

@@ -22,17 +22,27 @@ def test_library_exports_header_symbols():
     assert {s for s, _, _ in _lib.SIGNATURES} == set(syms)
 
 
-@pytest.mark.parametrize("model,launches", [
-    ("face_detection_short_range", 21), ("face_landmark", 25),
-    ("palm_detection_lite", 32), ("hand_landmark_lite", 37)])
-def test_plan_compiles_and_fuses(models_dir, model, launches):
+KINDS = ("gemm", "dw", "direct", "elt", "resize", "gap", "dwpw", "chain")
+
+
+@pytest.mark.parametrize("model,launches,chained", [
+    ("face_detection_short_range", 8, 14), ("face_landmark", 13, 13),
+    ("palm_detection_lite", 32, 0), ("hand_landmark_lite", 37, 0)])
+def test_plan_compiles_and_fuses(models_dir, model, launches, chained, monkeypatch):
     data = open(os.path.join(models_dir, model + ".onnx"), "rb").read()
     txt = _lib.plan_describe(data)
-    steps = [l for l in txt.splitlines() if l.split(" ")[0] in
-             ("gemm", "dw", "direct", "elt", "resize", "gap", "dwpw")]
+    steps = [l for l in txt.splitlines() if l.split(" ")[0] in KINDS]
     assert len(steps) == launches
     # no standalone element-wise pass survives: residual/pad/pool/act are all fused
     assert not [l for l in steps if l.startswith("elt")]
+    # the low-resolution tail runs as one chain launch (chain.hip); ZARU_HIP_FUSE=0 keeps
+    # the layer-per-launch plan (the chain replaces exactly `chained` of its launches)
+    ops = sum(int(l.split("ops=")[1].split()[0]) for l in steps if l.startswith("chain"))
+    assert ops == chained
+    monkeypatch.setenv("ZARU_HIP_FUSE", "0")
+    plain = [l for l in _lib.plan_describe(data).splitlines() if l.split(" ")[0] in KINDS]
+    assert not [l for l in plain if l.startswith("chain")]
+    assert len(plain) == launches + chained - (1 if chained else 0)
 
 
 def test_plan_output_selection(models_dir):

@@ -3,6 +3,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <map>
 #include <set>
 
@@ -80,6 +82,8 @@ class Compiler {
     bool act_from_node(const OnnxNode &nd, int C, int Cpad, ActDesc &a);
     void finalize_outputs();
     void allocate();
+    void schedule_sinks();
+    void form_chains();
 };
 
 // ---------------------------------------------------------------- shape inference
@@ -736,7 +740,9 @@ void Compiler::allocate() {
     std::vector<int> first(ns, 1 << 30), last(ns, -1);
     for (size_t i = 0; i < P.steps.size(); i++) {
         const Step &s = P.steps[i];
-        for (const TRef *r : {&s.in, &s.in2, &s.out})
+        std::vector<const TRef *> refs = {&s.in, &s.in2, &s.out};
+        for (const TRef &r : s.chain_outs) refs.push_back(&r);
+        for (const TRef *r : refs)
             if (r->kind == 0 && r->id >= 0) {
                 first[r->id] = std::min(first[r->id], (int)i);
                 last[r->id] = std::max(last[r->id], (int)i);
@@ -768,6 +774,257 @@ void Compiler::allocate() {
         placed.push_back(id);
     }
     P.arena_per_image = round_up(arena, 64);
+}
+
+// ---------------------------------------------------------------- layer chains
+namespace {
+
+constexpr int kChainMaxOps = 24, kChainLdsFloats = 40960;  // 160 KiB per workgroup
+constexpr int kChainKC = 16;
+
+int64_t positions(const TRef &r) { return (int64_t)r.H * r.W; }
+
+// a step the chain kernel can run: depthwise 3x3 -> 1x1 blocks and plain 1x1 convs over
+// <= 256 positions and <= 128 channels, reading internal tensors only
+bool chain_step_ok(const Step &s) {
+    if (s.in.kind != 0 || (s.res_mode && s.in2.kind != 0) || s.out.kind == 1) return false;
+    if (positions(s.in) > 256 || positions(s.out) > 256 || s.M > 128 || s.K > 128) return false;
+    if (s.kind == S_DWPW) return s.kh == 3 && s.kw == 3 && (s.stride == 1 || s.stride == 2);
+    if (s.kind == S_GEMM) return s.KK == 1 && s.in.H == s.out.H && s.in.W == s.out.W;
+    return false;
+}
+
+int round4(int64_t v) { return (int)((v + 3) / 4 * 4); }
+
+}  // namespace
+
+// A step that writes only a graph output feeds nothing else.  Chainable ones move up to just
+// after the producer of their inputs (so the tensor they read dies sooner), the others move to
+// the end (so they do not split a run of chainable layers).
+void Compiler::schedule_sinks() {
+    std::vector<Step> &S = P.steps;
+    std::vector<Step> body, late;
+    for (auto &s : S) {
+        if (s.out.kind == 2 && !chain_step_ok(s)) late.push_back(s);
+        else body.push_back(s);
+    }
+    std::vector<Step> out;
+    std::vector<Step> pending;  // chainable sinks waiting for their inputs' producers
+    auto produced = [&](int id) {
+        for (auto &t : out)
+            if (t.out.kind == 0 && t.out.id == id) return true;
+        return false;
+    };
+    auto ready = [&](const Step &s) {
+        return (s.in.kind != 0 || produced(s.in.id)) && (!s.res_mode || s.in2.kind != 0 || produced(s.in2.id));
+    };
+    for (auto &s : body) {
+        if (s.out.kind == 2) {
+            if (ready(s)) {
+                // insert right after the last producer of its inputs
+                size_t pos = 0;
+                for (size_t i = 0; i < out.size(); i++)
+                    if (out[i].out.kind == 0 && (out[i].out.id == s.in.id || (s.res_mode && out[i].out.id == s.in2.id)))
+                        pos = i + 1;
+                out.insert(out.begin() + pos, s);
+            } else {
+                pending.push_back(s);
+            }
+            continue;
+        }
+        out.push_back(s);
+    }
+    for (auto &s : pending) out.push_back(s);
+    for (auto &s : late) out.push_back(s);
+    S = std::move(out);
+}
+
+// Replace every maximal run (>= 2 steps) of chainable steps whose activations fit in LDS by
+// one S_CHAIN step.  LDS: the entry tensor and every tensor produced and consumed inside the
+// run get regions by liveness (a stride-1 layer may write over the input it consumes last);
+// tensors consumed after the run, and graph outputs, are written to their global homes.
+void Compiler::form_chains() {
+    std::vector<Step> &S = P.steps;
+    struct Alloc {
+        std::vector<int> off;  // per op: out region (-1: none)
+        std::map<int, int> where;  // storage id -> LDS offset
+        int end = 0, e_off = 0;
+        bool ok = false;
+    };
+    // LDS layout of steps [i, j] with entry tensor `entry`
+    auto layout = [&](size_t i, size_t j, const TRef &entry) {
+        Alloc A;
+        std::map<int, int> last;  // storage id -> last op index reading it within [i, j]
+        for (size_t k = i; k <= j; k++) {
+            last[S[k].in.id] = (int)k;
+            if (S[k].res_mode) last[S[k].in2.id] = (int)k;
+        }
+        struct Reg {
+            int off, size, id;
+        };
+        std::vector<Reg> live;
+        auto place = [&](int size, int prefer) {
+            std::sort(live.begin(), live.end(), [](const Reg &a, const Reg &b) { return a.off < b.off; });
+            auto fits = [&](int o) {
+                for (auto &r : live)
+                    if (o < r.off + r.size && r.off < o + size) return false;
+                return true;
+            };
+            if (prefer >= 0 && fits(prefer)) return prefer;
+            int o = 0;
+            for (auto &r : live) {
+                if (o + size <= r.off) break;
+                o = std::max(o, r.off + r.size);
+            }
+            return o;
+        };
+        auto release = [&](int id) {
+            live.erase(std::remove_if(live.begin(), live.end(), [&](const Reg &r) { return r.id == id; }), live.end());
+        };
+        const int esz = round4((int64_t)entry.C * positions(entry));
+        A.e_off = 0;
+        live.push_back({0, esz, entry.id});
+        A.where[entry.id] = 0;
+        A.end = esz;
+        for (size_t k = i; k <= j; k++) {
+            const Step &s = S[k];
+            if (!A.where.count(s.in.id) || (s.res_mode && !A.where.count(s.in2.id))) return A;  // input not in LDS
+            const bool used_later = s.out.kind == 0 && [&] {
+                for (size_t t = k + 1; t <= j; t++)
+                    if (S[t].in.id == s.out.id || (S[t].res_mode && S[t].in2.id == s.out.id)) return true;
+                return false;
+            }();
+            const bool same_p = positions(s.in) == positions(s.out) && s.stride == 1;
+            int prefer = -1;
+            if (same_p && last[s.in.id] == (int)k && (!s.res_mode || s.in2.id == s.in.id)) {
+                prefer = A.where[s.in.id];  // overwrite the consumed input
+                release(s.in.id);
+            }
+            int off = -1;
+            if (used_later) {
+                const int sz = round4((int64_t)s.M * positions(s.out));
+                off = place(sz, prefer);
+                live.push_back({off, sz, s.out.id});
+                A.where[s.out.id] = off;
+                A.end = std::max(A.end, off + sz);
+            }
+            A.off.push_back(off);
+            for (auto it = last.begin(); it != last.end(); ++it)
+                if (it->second == (int)k) release(it->first);
+        }
+        A.ok = true;
+        return A;
+    };
+    auto d_stride = [](const Step &s) {
+        const int np = (int)((positions(s.out) + 15) / 16 * 16);
+        return np % 32 == 16 ? np : np + 16;
+    };
+    std::vector<Step> out;
+    for (size_t i = 0; i < S.size();) {
+        const Step &s0 = S[i];
+        const bool entry_ok = chain_step_ok(s0) && positions(s0.in) % 4 == 0 &&
+                              (int64_t)s0.in.C * positions(s0.in) <= 32768;
+        size_t best_j = i;
+        Alloc best;
+        if (entry_ok) {
+            for (size_t j = i; j < S.size() && j - i < (size_t)kChainMaxOps && chain_step_ok(S[j]); j++) {
+                Alloc A = layout(i, j, s0.in);
+                if (!A.ok) break;
+                int dmax = 0;
+                for (size_t k = i; k <= j; k++)
+                    if (S[k].kind == S_DWPW) dmax = std::max(dmax, d_stride(S[k]));
+                if (A.end + 2 * kChainKC * dmax > kChainLdsFloats) break;
+                best_j = j;
+                best = A;
+            }
+        }
+        if (!entry_ok || best_j - i < 1) {
+            out.push_back(S[i]);
+            i++;
+            continue;
+        }
+        // steps [i, best_j] become one chain
+        Step c;
+        c.kind = S_CHAIN;
+        c.name = "chain(" + S[i].name + " .. " + S[best_j].name + ")";
+        c.in = s0.in;
+        int dmax = 0;
+        for (size_t k = i; k <= best_j; k++)
+            if (S[k].kind == S_DWPW) dmax = std::max(dmax, d_stride(S[k]));
+        c.chain_e_off = best.e_off;
+        c.chain_d_off = (best.end + 3) / 4 * 4;
+        c.chain_d_buf = kChainKC * dmax;
+        c.chain_lds = c.chain_d_off + 2 * c.chain_d_buf;
+        c.bytes = 4.0 * (double)s0.in.C * positions(s0.in);
+        std::vector<ChainOp> ops;
+        for (size_t k = i; k <= best_j; k++) {
+            const Step &s = S[k];
+            ChainOp o{};
+            o.kind = s.kind == S_DWPW ? CHAIN_DWPW : CHAIN_PW;
+            o.in_off = best.where[s.in.id];
+            o.res_off = s.res_mode ? best.where[s.in2.id] : -1;
+            o.out_off = best.off[k - i];
+            o.Cin = s.K;
+            o.Cout = s.M;
+            o.P = (int)positions(s.in);
+            o.W = s.in.W;
+            o.OP = (int)positions(s.out);
+            o.OW = s.out.W;
+            o.stride = s.stride;
+            o.pad_t = s.pad_t;
+            o.pad_l = s.pad_l;
+            o.Mpad = s.Mpad;
+            // wave tiling: 8 waves as MS groups along M x (8 / MS) along N, 16x16 tiles
+            const int MT = (s.M + 15) / 16, NT = (o.OP + 15) / 16;
+            int best_cost = 1 << 30;
+            for (int ms : {1, 2, 4, 8}) {
+                const int mtw = (MT + ms - 1) / ms, ntw = (NT + 8 / ms - 1) / (8 / ms);
+                if (mtw > 4 || ntw > 4 || mtw * ntw >= best_cost) continue;
+                best_cost = mtw * ntw;
+                o.MS = ms;
+                o.MTW = mtw;
+                o.NTW = ntw;
+            }
+            o.NT = NT;
+            if (best_cost == (1 << 30)) return;  // cannot tile: keep the plan unchained
+            o.res_mode = s.res_mode;
+            o.r_C = s.r_C;
+            o.res_P = s.res_mode ? (int)positions(s.in2) : 0;
+            o.res_W = s.res_mode ? s.in2.W : 0;
+            o.w_off = (int)s.w_off;
+            o.b_off = (int)s.b_off;
+            o.dw_w_off = (int)s.dw_w_off;
+            o.dw_b_off = (int)s.dw_b_off;
+            auto act = [](const ActDesc &a) {
+                return ChainAct{a.kind, a.lo, a.hi, (int)a.slope_off};
+            };
+            o.pre = act(s.pre);
+            o.post = act(s.post);
+            o.dw_act = act(s.dw_act);
+            o.ds = s.kind == S_DWPW ? d_stride(s) : 0;
+            // a global destination: graph outputs, and internal tensors read after the chain
+            bool exported = false;
+            if (s.out.kind == 0)
+                for (size_t t = best_j + 1; t < S.size(); t++)
+                    if (S[t].in.id == s.out.id || (S[t].res_mode && S[t].in2.id == s.out.id)) exported = true;
+            o.gout = -1;
+            if (s.out.kind == 2 || exported) {
+                if (c.chain_outs.size() >= (size_t)CHAIN_MAX_OUTS) return;
+                o.gout = (int)c.chain_outs.size();
+                c.chain_outs.push_back(s.out);
+                c.bytes += 4.0 * (double)s.M * positions(s.out);
+            }
+            ops.push_back(o);
+            c.flops += s.flops;
+        }
+        std::vector<float> words(ops.size() * sizeof(ChainOp) / 4);
+        std::memcpy(words.data(), ops.data(), ops.size() * sizeof(ChainOp));
+        c.chain_ops_off = push_weights(words);
+        c.chain_nops = (int)ops.size();
+        out.push_back(c);
+        i = best_j + 1;
+    }
+    S = std::move(out);
 }
 
 bool Compiler::run(const std::vector<uint32_t> &sel) {
@@ -815,10 +1072,18 @@ bool Compiler::run(const std::vector<uint32_t> &sel) {
             for (auto &i : M.nodes[ni].in)
                 if (!i.empty()) vals[i].consumers++;
     if (!lower()) return false;
+    const char *fuse = std::getenv("ZARU_HIP_FUSE");  // "0": the unchained plan (verification)
+    if (!(fuse && fuse[0] == '0')) {
+        schedule_sinks();
+        form_chains();
+    }
     for (size_t oi = 0; oi < P.outputs.size(); oi++) {
         bool written = false;
-        for (auto &s : P.steps)
+        for (auto &s : P.steps) {
             if (s.out.kind == 2 && s.out.id == (int)oi) written = true;
+            for (auto &r : s.chain_outs)
+                if (r.kind == 2 && r.id == (int)oi) written = true;
+        }
         if (!written) return fail("output " + P.outputs[oi].name + " is never written");
     }
     for (auto &s : P.steps) {
@@ -1074,6 +1339,29 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook
             r.scale_y = s.scale_y;
             r.scale_x = s.scale_x;
             kname = launch_resize(r, stream);
+            break;
+        }
+        case S_CHAIN: {
+            ChainParams c{};
+            c.weights = W;
+            c.ops_off = (int)s.chain_ops_off;
+            c.nops = s.chain_nops;
+            Resolved e = resolve(s.in, plan, b);
+            c.entry = e.p;
+            c.e_sN = e.sN;
+            c.e_sC = e.sC;
+            c.e_C = s.in.C;
+            c.e_P = s.in.H * s.in.W;
+            c.e_off = s.chain_e_off;
+            c.N = b.N;
+            c.d_off = s.chain_d_off;
+            c.d_buf = s.chain_d_buf;
+            c.lds_floats = s.chain_lds;
+            for (size_t i = 0; i < s.chain_outs.size(); i++) {
+                Resolved o = resolve(s.chain_outs[i], plan, b);
+                c.gout[i] = ChainOut{const_cast<float *>(o.p), o.sN, o.sC, o.sP};
+            }
+            kname = launch_chain(c, stream);
             break;
         }
         case S_GAP: {

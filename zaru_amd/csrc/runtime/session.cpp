@@ -394,6 +394,12 @@ int zr_plan_describe(const uint8_t *onnx, size_t len, const uint32_t *out_sel, s
             t += line;
         }
         for (auto &st : plan.steps) {
+            if (st.kind == zr::S_CHAIN) {
+                snprintf(line, sizeof line, "chain in=%s ops=%d outs=%zu lds_floats=%d flops/img=%.0f bytes/img=%.0f\n",
+                         ref(st.in).c_str(), st.chain_nops, st.chain_outs.size(), st.chain_lds, st.flops, st.bytes);
+                t += line;
+                continue;
+            }
             snprintf(line, sizeof line,
                      "%s%s in=%s out=%s k=%dx%d s=%d M=%d K=%d KK=%d pre=%s post=%s res=%d rC=%d elt=%d off=%lld oN=%lld oC=%lld oP=%lld\n",
                      kinds[st.kind], st.stem ? " stem" : "", ref(st.in).c_str(), ref(st.out).c_str(), st.kh, st.kw, st.stride,

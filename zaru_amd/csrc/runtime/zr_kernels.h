@@ -172,6 +172,54 @@ struct DwPwParams {
     Act dw_act;
 };
 
+// ---------------------------------------------------------------- layer chains (chain.hip)
+// A run of consecutive low-resolution layers (depthwise 3x3 -> 1x1 BlazeBlocks and plain 1x1
+// convs, <= 256 positions and <= 128 channels per image) executed by ONE workgroup per image
+// with every activation in LDS: the chain reads its entry tensor from HBM once and writes only
+// the tensors consumed outside it (graph outputs, later layers).  The op table is compiled
+// into the session's weight buffer (all fields 32-bit, offsets in floats), so the kernel reads
+// it through the scalar cache; only the binding-dependent pointers travel as kernel arguments.
+enum ChainOpKind : int { CHAIN_DWPW = 0, CHAIN_PW = 1 };
+
+struct ChainAct {
+    int kind;
+    float lo, hi;
+    int slope_off;  // floats into the weight buffer, -1 when none
+};
+
+struct ChainOp {
+    int kind;
+    int in_off, res_off, out_off;   // LDS offsets (floats); res_off / out_off -1: none
+    int Cin, Cout, P, W, OP, OW;    // input channels / positions / width; output positions / width
+    int stride, pad_t, pad_l;       // depthwise geometry (CHAIN_DWPW)
+    int Mpad, MS, MTW, NTW, NT;     // 1x1 weights [Cin][Mpad]; wave tiling (16x16 MFMA tiles)
+    int res_mode, r_C, res_P, res_W;
+    int w_off, b_off, dw_w_off, dw_b_off;
+    ChainAct pre, post, dw_act;
+    int gout;                       // global destination index (-1: none)
+    int ds;                         // depthwise-output row stride in the D buffers (floats)
+};
+static_assert(sizeof(ChainOp) % 4 == 0, "ChainOp is a table of 32-bit words");
+
+constexpr int CHAIN_MAX_OUTS = 8;
+
+struct ChainOut {  // element (n, c, q) at p + n*sN + c*sC + q*sP
+    float *p;
+    int64_t sN, sC, sP;
+};
+
+struct ChainParams {
+    const float *weights;
+    int ops_off, nops;              // op table at weights + ops_off (floats)
+    const float *entry;             // entry tensor, CNHW: (n, c, p) at entry + n*e_sN + c*e_sC + p
+    int64_t e_sN, e_sC;
+    int e_C, e_P, e_off;            // channels, positions, LDS offset
+    int N;
+    int d_off, d_buf;               // D buffers: two of d_buf floats at LDS offset d_off
+    int lds_floats;
+    ChainOut gout[CHAIN_MAX_OUTS];
+};
+
 bool stem_supported(int cin, int k, int stride, int cout);
 bool dwpw_supported(int k, int stride);
 
@@ -191,5 +239,6 @@ const char *launch_preproc(const PreprocParams &p, hipStream_t s);
 const char *launch_candidates(const CandParams &p, hipStream_t s);
 const char *launch_stem(const StemParams &p, bool pre, hipStream_t s);
 const char *launch_dwpw(const DwPwParams &p, hipStream_t s);
+const char *launch_chain(const ChainParams &p, hipStream_t s);
 
 }  // namespace zr
