@@ -1,6 +1,6 @@
 """The kernel forms the launchers choose between compute the same arithmetic in the same order,
-so switching a form off (its ZR_* switch, read once per process) must not change one bit of any
-model output.  Each configuration runs in a child process (the switches are process-wide); the
+so switching a form (ZARU_HIP_FORMS, read once per process) must not change one bit of any model
+output.  Each configuration runs in a child process (the switches are process-wide); the
 batch is large enough that every form the default build picks is exercised (LDS-DMA staged
 VALU and MFMA forms, the windowed V4 taps, the image-row head GEMM).
 """
@@ -30,15 +30,16 @@ for model, s in (("face_detection_short_range", 128), ("face_landmark", 192),
 np.savez(sys.argv[2], **out)
 """
 
-# each switch turns one form off; "all" turns every one off together
+# each setting turns one form off ("-form") or the opt-in chain form on; "all_off" every form
 SWITCHES = {
-    "default": {},
-    "no_valu_db": {"ZR_VALU_DB": "0"},
-    "no_dma": {"ZR_DWPW_DMA": "0"},
-    "no_v4": {"ZR_DWPW_V4": "0", "ZR_DWPW_DMA": "0"},
-    "no_rows": {"ZR_GEMM_ROWS": "0"},
-    "dma_chunk32": {"ZR_DWPW_FKC": "32"},  # not an off-switch: the other DMA chunk size
-    "no_chain": {"ZARU_HIP_FUSE": "0"},    # the layer-per-launch plan (no chain.hip)
+    "default": "",
+    "no_valu_db": "-valu_db",
+    "no_valu": "-valu",
+    "no_dma": "-dma",
+    "no_v4": "-v4,-dma",
+    "no_rows": "-rows",
+    "chain": "+chain",  # low-resolution layer runs in one launch per image (chain.hip)
+    "all_off": "-dma,-v4,-valu,-valu_db,-rows",
 }
 
 
@@ -49,9 +50,7 @@ def outputs(tmp_path_factory):
     for name, env in SWITCHES.items():
         path = str(d / f"{name}.npz")
         e = dict(os.environ)
-        for k in ("ZR_VALU_DB", "ZR_DWPW_DMA", "ZR_DWPW_V4", "ZR_GEMM_ROWS", "ZR_DWPW_FKC", "ZARU_HIP_FUSE"):
-            e.pop(k, None)
-        e.update(env)
+        e["ZARU_HIP_FORMS"] = env
         subprocess.run([sys.executable, "-c", CHILD, REPO, path], env=e, check=True, timeout=110)
         with np.load(path) as z:
             res[name] = {k: z[k] for k in z.files}

@@ -2,10 +2,14 @@
 declares, and compiles every hot-path model into a fused launch plan (no GPU needed)."""
 import os
 import re
+import subprocess
+import sys
 
 import pytest
 
 from zaru_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _header_symbols():
@@ -25,24 +29,34 @@ def test_library_exports_header_symbols():
 KINDS = ("gemm", "dw", "direct", "elt", "resize", "gap", "dwpw", "chain")
 
 
+CHAINED_CHILD = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+from zaru_amd import _lib
+print(_lib.plan_describe(open(sys.argv[2], "rb").read()))
+"""
+
+
 @pytest.mark.parametrize("model,launches,chained", [
-    ("face_detection_short_range", 8, 14), ("face_landmark", 13, 13),
+    ("face_detection_short_range", 21, 14), ("face_landmark", 25, 13),
     ("palm_detection_lite", 32, 0), ("hand_landmark_lite", 37, 0)])
-def test_plan_compiles_and_fuses(models_dir, model, launches, chained, monkeypatch):
-    data = open(os.path.join(models_dir, model + ".onnx"), "rb").read()
-    txt = _lib.plan_describe(data)
+def test_plan_compiles_and_fuses(models_dir, model, launches, chained):
+    path = os.path.join(models_dir, model + ".onnx")
+    txt = _lib.plan_describe(open(path, "rb").read())
     steps = [l for l in txt.splitlines() if l.split(" ")[0] in KINDS]
     assert len(steps) == launches
     # no standalone element-wise pass survives: residual/pad/pool/act are all fused
     assert not [l for l in steps if l.startswith("elt")]
-    # the low-resolution tail runs as one chain launch (chain.hip); ZARU_HIP_FUSE=0 keeps
-    # the layer-per-launch plan (the chain replaces exactly `chained` of its launches)
-    ops = sum(int(l.split("ops=")[1].split()[0]) for l in steps if l.startswith("chain"))
+    assert not [l for l in steps if l.startswith("chain")]  # chains are opt-in
+    # with the chain form on (ZARU_HIP_FORMS=+chain, read once per process: a child process)
+    # the low-resolution tail runs as one chain launch replacing exactly `chained` launches
+    env = dict(os.environ, ZARU_HIP_FORMS="+chain")
+    out = subprocess.run([sys.executable, "-c", CHAINED_CHILD, REPO, path], env=env, check=True,
+                         capture_output=True, text=True, timeout=120).stdout
+    fused = [l for l in out.splitlines() if l.split(" ")[0] in KINDS]
+    ops = sum(int(l.split("ops=")[1].split()[0]) for l in fused if l.startswith("chain"))
     assert ops == chained
-    monkeypatch.setenv("ZARU_HIP_FUSE", "0")
-    plain = [l for l in _lib.plan_describe(data).splitlines() if l.split(" ")[0] in KINDS]
-    assert not [l for l in plain if l.startswith("chain")]
-    assert len(plain) == launches + chained - (1 if chained else 0)
+    assert len(fused) == launches - chained + (1 if chained else 0)
 
 
 def test_plan_output_selection(models_dir):

@@ -402,10 +402,11 @@ void DetectTrackPipeline::step(bool more) {
         const auto t1 = clk::now();
         stage_decode_and_rois(s, frames, forced_);
         times_.decode_nms_ms += ms_since(t1);
+        // the next run's detections of this slot queue behind its landmarks at once, so the
+        // GPU has them while the host decodes the later slots (the slot's detector outputs and
+        // letterbox views are consumed; the landmark launch copied its view descriptors)
+        if (more) stage_detect(s, frames);
     }
-    // the next run's detections queue behind this run's landmarks on each slot's stream
-    if (more)
-        for (size_t k = 0; k < S; k++) stage_detect(*slots_[k], frames);
     for (size_t k = 0; k < S; k++) {
         Slot &s = *slots_[k];
         const auto t = clk::now();

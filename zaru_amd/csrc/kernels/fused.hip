@@ -349,129 +349,6 @@ __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) 
     }
 }
 
-// Row-staged variant for the high-resolution, few-channel layers (planes of >= 128 positions,
-// <= 96 output channels), where the tap-per-lane form above is VALU-bound on address math and
-// padding masks.  A tile is 128 consecutive positions of ONE image; per chunk of RFKC channels
-// the input rows those positions need (full padded width, zeros where the ONNX padding is) are
-// staged in LDS with coalesced row loads, and each depthwise tap is then one ds_read plus one FMA.
-constexpr int RBN = 128, RFKC = 8;
-
-template <int K, int S, int MT>
-__global__ __launch_bounds__(256) void dwpw_rows_kernel(const DwPwParams P, int tpi, int ntiles, int rmax) {
-    constexpr int PER = RFKC / 2;  // depthwise outputs per thread per chunk (2 channels in parallel)
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const GemmParams &G = P.g;
-    const int Wp = (P.OW - 1) * S + K;          // staged row width (covers every tap)
-    float *sIn = smem;                          // [RFKC][rmax][Wp]
-    float *sD = sIn + RFKC * rmax * Wp;         // [RFKC][RBN]
-    float *sW = sD + RFKC * RBN;                // [RFKC][MT*32]
-
-    const int cpx = gridDim.x >> 3;  // gridDim.x is a multiple of 8
-    const int tile = (blockIdx.x & 7) * cpx + (blockIdx.x >> 3);
-    if (tile >= ntiles) return;  // whole workgroup, before any barrier
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int kh = lane >> 5, col = lane & 31;
-    const int n = tile / tpi, q0 = (tile - n * tpi) * RBN;
-    const int Pq = G.P, H = P.in.H, W = P.in.W, Cin = G.K;
-    const int oy_a = q0 / P.OW, oy_b = min(q0 + RBN - 1, Pq - 1) / P.OW;
-    const int iy_a = oy_a * S - P.pad_t;
-    const int R = (oy_b - oy_a) * S + K;  // <= rmax
-
-    // depthwise role: position dq of the tile, channels dc, dc + 2, ... of each chunk
-    const int dq = tid & (RBN - 1);
-    const int dc = __builtin_amdgcn_readfirstlane(tid >> 7);
-    const int qd = min(q0 + dq, Pq - 1);
-    const int oy = qd / P.OW, ox = qd - oy * P.OW;
-    const int lb = (oy * S - P.pad_t - iy_a) * Wp + ox * S;  // staged index of tap (0, 0)
-    const uint32_t nbase = (uint32_t)n * (uint32_t)P.in.sN;
-
-    f32x16 acc[MT];
-#pragma unroll
-    for (int t = 0; t < MT; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-
-    for (int kc = 0; kc < Cin; kc += RFKC) {
-        // 1. stage rows iy_a .. iy_a + R - 1 of RFKC channels: a wave per row, lanes along x
-        //    (Wp <= 128: two loads per lane per row), 4 rows per wave in flight at once
-        const int nrows = RFKC * R;
-        for (int row0 = wave; row0 < nrows; row0 += 16) {
-            float v[4][2];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int row = min(row0 + 4 * k, nrows - 1);
-                const int c = row / R, r = row - c * R;
-                const int ch = kc + c < Cin ? kc + c : Cin - 1;
-                const int iy = iy_a + r;
-                const bool rok = iy >= 0 && iy < H && kc + c < Cin;
-                const float *src = P.in.p + (size_t)(uint32_t)ch * (uint32_t)P.in.sC;
-                const uint32_t rowoff = nbase + (uint32_t)(rok ? iy : 0) * (uint32_t)W;
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int ix = lane + 64 * h - P.pad_l;
-                    const bool ok = rok && ix >= 0 && ix < W;
-                    const float x = src[rowoff + (uint32_t)(ok ? ix : 0)];
-                    v[k][h] = ok ? x : 0.f;
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int row = row0 + 4 * k;
-                if (row >= nrows) break;
-                const int c = row / R, r = row - c * R;
-                float *dst = sIn + (c * rmax + r) * Wp;
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (lane + 64 * h < Wp) dst[lane + 64 * h] = v[k][h];
-            }
-        }
-        // 2. the chunk of the transposed 1x1 weights
-        for (int i = tid; i < RFKC * MT * 32; i += 256) {
-            const int r = i / (MT * 32), cc = i - r * (MT * 32);
-            const int k = kc + r;
-            sW[i] = (k < Cin && cc < G.Mpad) ? G.wt[(int64_t)k * G.Mpad + cc] : 0.f;
-        }
-        __syncthreads();
-        // 3. depthwise from LDS
-        float dv[PER];
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int c = dc + 2 * i;
-            const int cl = kc + c < Cin ? kc + c : Cin - 1;
-            const float *w = P.dw_w + cl * (K * K);
-            const float *t0 = sIn + c * rmax * Wp + lb;
-            float a = P.dw_b[cl];
-#pragma unroll
-            for (int ky = 0; ky < K; ++ky)
-#pragma unroll
-                for (int kx = 0; kx < K; ++kx) a = __builtin_fmaf(w[ky * K + kx], t0[ky * Wp + kx], a);
-            dv[i] = a;
-        }
-        apply_act_n<PER>(P.dw_act, dv, [&](int i) {
-            const int c = kc + dc + 2 * i;
-            return c < Cin ? c : Cin - 1;
-        });
-#pragma unroll
-        for (int i = 0; i < PER; ++i) sD[(dc + 2 * i) * RBN + dq] = kc + dc + 2 * i < Cin ? dv[i] : 0.f;
-        __syncthreads();
-        // 4. the 1x1 conv over the chunk
-#pragma unroll
-        for (int s = 0; s < RFKC / 2; ++s) {
-            const float b = sD[(2 * s + kh) * RBN + wave * 32 + col];
-#pragma unroll
-            for (int t = 0; t < MT; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(sW[(2 * s + kh) * (MT * 32) + t * 32 + col], b,
-                                                              acc[t], 0, 0, 0);
-        }
-        __syncthreads();
-    }
-
-    const int q = q0 + wave * 32 + col;
-    if (q >= Pq) return;
-#pragma unroll
-    for (int t = 0; t < MT; ++t) epilogue_tile(G, acc[t], n, q, t * 32, kh);
-}
-
 // VALU form for the high-resolution layers with few channels (Cin * Cout <= 2048: the
 // BlazeBlocks at 96^2 .. 32^2), where the MFMA tile would be mostly padding and the
 // per-lane tap loads cost more memory instructions than the bytes they bring.  One thread per
@@ -662,129 +539,6 @@ __global__ __launch_bounds__(256) void dwpw_valu_kernel(const DwPwParams P, int 
         if (m < G.M) G.out[ob + (uint32_t)m * (uint32_t)G.o_sC] = v[m];
 }
 
-// Image-tile MFMA form for the low-resolution layers (planes of <= 256 positions: 16^2 ... 3^2,
-// with up to 256 channels).  A workgroup owns G whole images (G * P <= 256 columns), so the
-// depthwise input of a channel chunk is the contiguous run of G * P floats of each channel
-// (CNHW): it is copied into zero-bordered LDS planes once, and each tap is then one ds_read.
-// The 1x1 conv runs as v_mfma_f32_32x32x2_f32 with the 4 waves along N (NTW 32-column tiles
-// each) and all MT row tiles per wave; Mpad > MT*32 splits M across workgroups.
-constexpr int IFKC = 16, IBN = 256;
-
-template <int K, int S, int MT, int NTW>
-__global__ __launch_bounds__(256) void dwpw_img_kernel(const DwPwParams P, int G, int ntiles, int nimg) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const GemmParams &G_ = P.g;
-    const int H = P.in.H, W = P.in.W, Pin = H * W, Pq = G_.P, OW = P.OW;
-    const int Hp = (P.OW == 0) ? 0 : ((Pq / OW) - 1) * S + K, Wp = (OW - 1) * S + K;  // padded plane
-    const int plane = Hp * Wp;
-    float *sIn = smem;                         // [IFKC][G][Hp][Wp]
-    float *sD = sIn + IFKC * G * plane;        // [IFKC][IBN]
-    float *sW = sD + IFKC * IBN;               // [IFKC][MT*32]
-
-    const int cpx = gridDim.x >> 3;  // gridDim.x is a multiple of 8
-    const int tile = (blockIdx.x & 7) * cpx + (blockIdx.x >> 3);
-    if (tile >= ntiles) return;  // whole workgroup, before any barrier
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int kh = lane >> 5, col = lane & 31;
-    const int n0 = tile * G, g_here = min(G, nimg - n0);
-    const int cols = g_here * Pq;
-    const int m0 = blockIdx.y * (MT * 32);
-    const int Cin = G_.K;
-
-    // zero every staged plane once: the borders (ONNX padding) are never written again
-    for (int i = tid; i < IFKC * G * plane; i += 256) sIn[i] = 0.f;
-    // depthwise role: column dq (image g, position q), all IFKC channels of each chunk
-    const int dq = min(tid, cols - 1);
-    const int dg = dq / Pq, dqq = dq - dg * Pq;
-    const int oy = dqq / OW, ox = dqq - oy * OW;
-    const int lb = dg * plane + (oy * S) * Wp + ox * S;  // staged index of tap (0, 0)
-    const int pt = P.pad_t, pl = P.pad_l;
-    const float inv_W = 1.f / (float)W, inv_Pin = 1.f / (float)Pin;
-
-    f32x16 acc[MT][NTW];
-#pragma unroll
-    for (int t = 0; t < MT; ++t)
-#pragma unroll
-        for (int u = 0; u < NTW; ++u)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
-
-    const int run = g_here * Pin;  // contiguous floats per channel for this tile
-    for (int kc = 0; kc < Cin; kc += IFKC) {
-        __syncthreads();  // previous chunk's readers are done with sIn / sW
-        // 1. copy the chunk's channel runs into the interiors of the padded planes
-        const int total = IFKC * run;
-        for (int base = 0; base < total; base += 256 * 8) {
-            float v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int e = min(base + tid + 256 * u, total - 1);
-                const int c = e / run, r = e - c * run;
-                const int ch = kc + c < Cin ? kc + c : Cin - 1;
-                v[u] = P.in.p[(size_t)(uint32_t)ch * (uint32_t)P.in.sC + (uint32_t)n0 * (uint32_t)P.in.sN + (uint32_t)r];
-                v[u] = kc + c < Cin ? v[u] : 0.f;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int e = base + tid + 256 * u;
-                if (e < total) {
-                    const int c = e / run, r = e - c * run;
-                    const int g = qdiv(r, Pin, inv_Pin), rr = r - g * Pin;
-                    const int iy = qdiv(rr, W, inv_W), ix = rr - iy * W;
-                    sIn[(c * G + g) * plane + (iy + pt) * Wp + ix + pl] = v[u];
-                }
-            }
-        }
-        for (int i = tid; i < IFKC * MT * 32; i += 256) {
-            const int r = i / (MT * 32), cc = i - r * (MT * 32);
-            const int k = kc + r, m = m0 + cc;
-            sW[i] = (k < Cin && m < G_.Mpad) ? G_.wt[(int64_t)k * G_.Mpad + m] : 0.f;
-        }
-        __syncthreads();
-        // 2. depthwise of all IFKC channels of this thread's column
-        float dv[IFKC];
-#pragma unroll
-        for (int c = 0; c < IFKC; ++c) {
-            const int cl = kc + c < Cin ? kc + c : Cin - 1;
-            const float *w = P.dw_w + cl * (K * K);
-            const float *t0 = sIn + c * G * plane + lb;
-            float a = P.dw_b[cl];
-#pragma unroll
-            for (int ky = 0; ky < K; ++ky)
-#pragma unroll
-                for (int kx = 0; kx < K; ++kx) a = __builtin_fmaf(w[ky * K + kx], t0[ky * Wp + kx], a);
-            dv[c] = a;
-        }
-        apply_act_n<IFKC>(P.dw_act, dv, [&](int c) { return kc + c < Cin ? kc + c : Cin - 1; });
-#pragma unroll
-        for (int c = 0; c < IFKC; ++c) sD[c * IBN + tid] = (kc + c < Cin && tid < cols) ? dv[c] : 0.f;
-        __syncthreads();
-        // 3. the 1x1 conv over the chunk
-#pragma unroll
-        for (int s = 0; s < IFKC / 2; ++s) {
-            float a[MT], b[NTW];
-#pragma unroll
-            for (int t = 0; t < MT; ++t) a[t] = sW[(2 * s + kh) * (MT * 32) + t * 32 + col];
-#pragma unroll
-            for (int u = 0; u < NTW; ++u) b[u] = sD[(2 * s + kh) * IBN + (wave * NTW + u) * 32 + col];
-#pragma unroll
-            for (int t = 0; t < MT; ++t)
-#pragma unroll
-                for (int u = 0; u < NTW; ++u)
-                    acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t], b[u], acc[t][u], 0, 0, 0);
-        }
-    }
-
-#pragma unroll
-    for (int u = 0; u < NTW; ++u) {
-        const int c = (wave * NTW + u) * 32 + col;
-        if (c >= cols) continue;
-        const int g = c / Pq, q = c - g * Pq;
-#pragma unroll
-        for (int t = 0; t < MT; ++t) epilogue_tile(G_, acc[t][u], n0 + g, q, m0 + t * 32, kh);
-    }
-}
-
 // LDS-DMA form of the MFMA dwpw for the stride-1 low-resolution layers (24^2 ... 6^2 planes
 // with 64-256 channels), whose register-staged form waits on memory most of the time.  Per
 // chunk of DFKC input channels one buffer receives, by global_load_lds_dwordx4 (no VGPRs, no
@@ -944,12 +698,8 @@ constexpr DwPwLayout kLayouts[] = {{1, 1, 1}, {1, 2, 1}, {1, 3, 1}, {1, 4, 1}, {
 // The V4 depthwise form (see dwpw_kernel) applies when rows split into aligned quads and the
 // layer uses the models' TF-style pads.
 static bool v4_ok(const DwPwParams &p) {
-    static const int mode = [] {  // ZR_DWPW_V4=0 disables the form (A/B runs)
-        const char *e = std::getenv("ZR_DWPW_V4");
-        return e ? std::atoi(e) : 1;
-    }();
     const int pl = p.stride == 1 ? p.k / 2 : p.k / 2 - 1;
-    return mode && p.OW % 4 == 0 && p.in.W % 4 == 0 && p.pad_l == pl && p.pad_t == pl &&
+    return form_on(FORM_V4) && p.OW % 4 == 0 && p.in.W % 4 == 0 && p.pad_l == pl && p.pad_t == pl &&
            p.g.ncols % 4 == 0 && p.g.P % 4 == 0;
 }
 
@@ -957,14 +707,10 @@ static bool v4_ok(const DwPwParams &p) {
 // input run any BN-column tile needs, rounded to 16 B, and whole 1 KiB DMA wave-instructions.
 template <int K, int S, int WM, int MTW, int DFKC>
 static size_t dma_plan(const DwPwParams &p, int *runmax, int *bufsz) {
-    static const int mode = [] {  // ZR_DWPW_DMA=0 disables the form, 1 limits it to stride 1
-        const char *e = std::getenv("ZR_DWPW_DMA");
-        return e ? std::atoi(e) : 2;
-    }();
     constexpr int BN = (4 / WM) * 32, BM = WM * MTW * 32, KKP = (DFKC * K * K + 3) / 4 * 4;
     const int H = p.in.H, W = p.in.W, Pin = H * W, Pq = p.g.P, OW = p.OW;
     const int nimg = p.g.ncols / Pq;
-    if (!mode || (S == 2 && mode < 2) || p.in.sN != Pin || p.in.sC % 4 || ((int64_t)nimg * Pin) % 4 || p.g.K % 4 ||
+    if (!form_on(FORM_DMA) || p.in.sN != Pin || p.in.sC % 4 || ((int64_t)nimg * Pin) % 4 || p.g.K % 4 ||
         ((uintptr_t)p.in.p | (uintptr_t)p.g.wt | (uintptr_t)p.dw_w | (uintptr_t)p.dw_b) % 16)
         return 0;
     int rm = 0;
@@ -990,22 +736,10 @@ const char *dwpw_go(const DwPwParams &p, hipStream_t s) {
     const int nct = (p.g.ncols + BN - 1) / BN;
     const int mb = (p.g.Mpad + BM - 1) / BM;
     dim3 grid((nct + 7) / 8 * 8, mb);
-    {
-        // input channels per DMA chunk (ZR_DWPW_FKC=32: half the chunk barriers, twice the LDS)
-        static const int fkc = [] {
-            const char *e = std::getenv("ZR_DWPW_FKC");
-            return e && std::atoi(e) == 32 ? 32 : 16;
-        }();
-        int runmax = 0, bufsz = 0;
-        if (fkc == 32) {
-            if (const size_t lds = dma_plan<K, S, WM, MTW, 32>(p, &runmax, &bufsz)) {
-                hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, 32>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
-                return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,32>", K, S, WM, MTW);
-            }
-        } else if (const size_t lds = dma_plan<K, S, WM, MTW, 16>(p, &runmax, &bufsz)) {
-            hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, 16>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
-            return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,16>", K, S, WM, MTW);
-        }
+    int runmax = 0, bufsz = 0;
+    if (const size_t lds = dma_plan<K, S, WM, MTW, 16>(p, &runmax, &bufsz)) {
+        hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, 16>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
+        return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,16>", K, S, WM, MTW);
     }
     const bool v4 = v4_ok(p);
     if (v4) hipLaunchKernelGGL((dwpw_kernel<K, S, WM, MTW, 1, true>), grid, dim3(256), 0, s, p, nct);
@@ -1028,35 +762,6 @@ const char *dwpw_layout(const DwPwParams &p, const DwPwLayout &l, hipStream_t s)
     }
 }
 
-}  // namespace
-
-namespace {
-
-template <int K, int S, int MT>
-const char *dwpw_rows_go(const DwPwParams &p, hipStream_t s) {
-    const int P = p.g.P, tpi = (P + RBN - 1) / RBN, ntiles = tpi * p.g.ncols / P;
-    // the most input rows any tile needs
-    int rmax = 0;
-    for (int t = 0; t < tpi; t++) {
-        const int q0 = t * RBN, a = q0 / p.OW, b = std::min(q0 + RBN - 1, P - 1) / p.OW;
-        rmax = std::max(rmax, (b - a) * S + K);
-    }
-    const int Wp = (p.OW - 1) * S + K;
-    const size_t lds = sizeof(float) * ((size_t)RFKC * rmax * Wp + RFKC * RBN + RFKC * MT * 32);
-    dim3 grid((ntiles + 7) / 8 * 8);
-    hipLaunchKernelGGL((dwpw_rows_kernel<K, S, MT>), grid, dim3(256), lds, s, p, tpi, ntiles, rmax);
-    return kernel_name("dwpw_rows_kernel<%d,%d,%d>", K, S, MT);
-}
-
-template <int K, int S>
-const char *dwpw_rows_mt(const DwPwParams &p, hipStream_t s) {
-    switch (p.g.Mpad / 32) {
-    case 1: return dwpw_rows_go<K, S, 1>(p, s);
-    case 2: return dwpw_rows_go<K, S, 2>(p, s);
-    default: return dwpw_rows_go<K, S, 3>(p, s);
-    }
-}
-
 template <int K, int S, int CO>
 const char *dwpw_valu_go(const DwPwParams &p, hipStream_t s) {
     const int P = p.g.P, tpi = (P + VTQ - 1) / VTQ, ntiles = tpi * (p.g.ncols / P);
@@ -1066,18 +771,13 @@ const char *dwpw_valu_go(const DwPwParams &p, hipStream_t s) {
         rmax = std::max(rmax, (b - a) * S + K);
     }
     const int lw = p.in.W + 8;
-    // Double-buffered LDS-DMA staging (ZR_VALU_DB=0 disables it for A/B runs).  Measured per CO:
-    // 32 channels: 8-channel chunks while two buffers fit 64 KiB (the 131 VGPRs hold a CU to 3
-    // workgroups anyway), else 4-channel chunks; 16 channels: 4-channel chunks, so two buffers
-    // cost no more LDS (and occupancy) than one 8-channel buffer; 48 channels: only at stride 2
-    // (slower at stride 1; ZR_VALU_DB=2 takes it there too).
-    static const int db_mode = [] {
-        const char *e = std::getenv("ZR_VALU_DB");
-        return e ? std::atoi(e) : 1;
-    }();
+    // Double-buffered LDS-DMA staging (form valu_db).  Measured per CO: 32 channels: 8-channel
+    // chunks while two buffers fit 64 KiB (the 131 VGPRs hold a CU to 3 workgroups anyway), else
+    // 4-channel chunks; 16 channels: 4-channel chunks, so two buffers cost no more LDS (and
+    // occupancy) than one 8-channel buffer; 48 channels: only at stride 2 (slower at stride 1).
     auto buf_of = [&](int vf) { return (vf * rmax * lw + 255) / 256 * 256; };  // whole 1 KiB DMA rows
     const bool fit8 = 2 * sizeof(float) * (size_t)buf_of(VFKC) <= 64 * 1024;
-    const bool db = db_mode && (CO == 16 || CO == 32 || (CO == 48 && (S == 2 || db_mode == 2))) &&
+    const bool db = form_on(FORM_VALU_DB) && (CO == 16 || CO == 32 || (CO == 48 && S == 2)) &&
                     2 * sizeof(float) * (size_t)buf_of(4) <= 64 * 1024;
     const bool small = db && !(CO == 32 && fit8);
     const int vf = small ? 4 : VFKC;
@@ -1107,87 +807,25 @@ const char *dwpw_valu_co(const DwPwParams &p, hipStream_t s) {
 
 }  // namespace
 
-template <int K, int S, int MT>
-const char *dwpw_img_go(const DwPwParams &p, hipStream_t s) {
-    constexpr int NTW = IBN / 128;  // 4 waves x NTW x 32 = IBN columns
-    const int P = p.g.P, nimg = p.g.ncols / P, G = std::max(1, IBN / P);
-    const int ntiles = (nimg + G - 1) / G, mb = (p.g.Mpad + MT * 32 - 1) / (MT * 32);
-    const int Hp = (P / p.OW - 1) * S + K, Wp = (p.OW - 1) * S + K;
-    const size_t lds = sizeof(float) * ((size_t)IFKC * G * Hp * Wp + IFKC * IBN + IFKC * MT * 32);
-    dim3 grid((ntiles + 7) / 8 * 8, mb);
-    hipLaunchKernelGGL((dwpw_img_kernel<K, S, MT, NTW>), grid, dim3(256), lds, s, p, G, ntiles, nimg);
-    return kernel_name("dwpw_img_kernel<%d,%d,%d,%d>", K, S, MT, NTW);
-}
-
-template <int K, int S>
-const char *dwpw_img_mt(const DwPwParams &p, hipStream_t s) {
-    switch (std::min(4, p.g.Mpad / 32)) {
-    case 1: return dwpw_img_go<K, S, 1>(p, s);
-    case 2: return dwpw_img_go<K, S, 2>(p, s);
-    case 3: return dwpw_img_go<K, S, 3>(p, s);
-    default: return dwpw_img_go<K, S, 4>(p, s);
-    }
-}
-
-// The image-tile form applies to planes of <= IBN positions whose padded staging fits in
-// 96 KiB (the depthwise input plane must be exactly the output plane's receptive area).
-static bool img_form(const DwPwParams &p) {
-    static const int mode = [] {  // opt-in (ZR_DWPW_IMG=1): slower than dwpw_kernel so far
-        const char *e = std::getenv("ZR_DWPW_IMG");
-        return e ? std::atoi(e) : 0;
-    }();
-    const int P = p.g.P;
-    if (mode == 5 && p.k != 5) return false;  // ZR_DWPW_IMG=5: 5x5 layers only
-    // the tile's images must be one contiguous run per channel (CNHW activations)
-    if (!mode || P > IBN || p.g.ncols % P != 0 || P % p.OW != 0 || p.in.sN != (int64_t)p.in.H * p.in.W)
-        return false;
-    const int OH = P / p.OW, Hp = (OH - 1) * p.stride + p.k, Wp = (p.OW - 1) * p.stride + p.k;
-    // every input pixel must land inside the padded plane (no cropping)
-    if (p.pad_t + p.in.H > Hp || p.pad_l + p.in.W > Wp) return false;
-    const int G = std::max(1, IBN / P);
-    return sizeof(float) * ((size_t)IFKC * G * Hp * Wp + IFKC * IBN + IFKC * 128) <= 96 * 1024;
-}
-
 // The VALU form applies to (see dwpw_valu_kernel): >= 256 positions per image, W % 4 == 0
 // (16-byte row loads), Cout <= 48, Cin * Cout <= 2048, staged rows within 64 KiB.
 static bool valu_form(const DwPwParams &p) {
-    static const int mode = [] {  // ZR_DWPW_VALU=0 disables the form (A/B runs)
-        const char *e = std::getenv("ZR_DWPW_VALU");
-        return e ? std::atoi(e) : 1;
-    }();
-    if (!mode || p.g.P < VTQ || p.in.W % 4 != 0 || p.in.W > 248 || p.g.M > 48 || p.g.K * p.g.M > 2048)
+    if (!form_on(FORM_VALU) || p.g.P < VTQ || p.in.W % 4 != 0 || p.in.W > 248 || p.g.M > 48 || p.g.K * p.g.M > 2048)
         return false;
     if (p.g.ncols % p.g.P != 0) return false;
     const int rows = (VTQ / p.OW + 2) * p.stride + p.k;
     return sizeof(float) * (size_t)VFKC * rows * (p.in.W + 8) <= 64 * 1024;
 }
 
-// Layout choice.  High-resolution planes with few channels take the VALU form; otherwise
-// (MFMA form) high-resolution planes with few output channels may take the row-staged kernel.
-// Otherwise: no M split unless Mpad > 256, at most 1/3 padded rows; among those, the widest
+// Layout choice.  High-resolution planes with few channels take the VALU form; otherwise (MFMA
+// form): no M split unless Mpad > 256, at most 1/3 padded rows; among those, the widest
 // column tile that still gives >= 4 workgroups per CU (else the most workgroups).
 const char *launch_dwpw(const DwPwParams &p, hipStream_t s) {
-    static const bool rows_on = [] {  // A/B switch while the staged form is being tuned
-        const char *e = std::getenv("ZR_DWPW_ROWS");
-        return e && e[0] == '1';
-    }();
     if (valu_form(p)) {
         if (p.k == 3) return p.stride == 1 ? dwpw_valu_co<3, 1>(p, s) : dwpw_valu_co<3, 2>(p, s);
         return p.stride == 1 ? dwpw_valu_co<5, 1>(p, s) : dwpw_valu_co<5, 2>(p, s);
     }
-    if (img_form(p)) {
-        if (p.k == 3) return p.stride == 1 ? dwpw_img_mt<3, 1>(p, s) : dwpw_img_mt<3, 2>(p, s);
-        return p.stride == 1 ? dwpw_img_mt<5, 1>(p, s) : dwpw_img_mt<5, 2>(p, s);
-    }
-    const int Wp = (p.OW - 1) * p.stride + p.k;
-    if (rows_on && p.g.P >= RBN && p.g.Mpad <= 96 && Wp <= 128 && p.g.ncols % p.g.P == 0) {
-        if (p.k == 3) return p.stride == 1 ? dwpw_rows_mt<3, 1>(p, s) : dwpw_rows_mt<3, 2>(p, s);
-        return p.stride == 1 ? dwpw_rows_mt<5, 1>(p, s) : dwpw_rows_mt<5, 2>(p, s);
-    }
-    static const int64_t min_wgs = [] {  // workgroups one launch should reach (ZR_DWPW_MINWG)
-        const char *e = std::getenv("ZR_DWPW_MINWG");
-        return e ? (int64_t)std::atoll(e) : (int64_t)1024;
-    }();
+    constexpr int64_t min_wgs = 1024;  // workgroups one launch should reach
     const DwPwLayout *best = nullptr;
     int64_t best_wgs = 0;
     for (const DwPwLayout &l : kLayouts) {

@@ -294,14 +294,6 @@ static const char *launch_mt(const GemmParams &p, dim3 grid, hipStream_t s) {
     return names[p.KK > 1][MT];
 }
 
-static bool rows_form() {  // ZR_GEMM_ROWS=0 disables the image-row form (A/B runs)
-    static const int mode = [] {
-        const char *e = std::getenv("ZR_GEMM_ROWS");
-        return e ? std::atoi(e) : 1;
-    }();
-    return mode != 0;
-}
-
 const char *launch_gemm(const GemmParams &p, hipStream_t s) {
     const int mtiles = p.Mpad / 32;
     // LDS-tiled path: X must be a row-major [K][ncols] matrix with 16-B aligned rows
@@ -318,7 +310,7 @@ const char *launch_gemm(const GemmParams &p, hipStream_t s) {
         while (mt > 1 && (int64_t)((p.ncols + bn - 1) / bn) * ((mtiles + mt - 1) / mt) < 512) --mt;
         return nt == 2 ? launch_tiled_nt<2>(p, mt, s) : launch_tiled_nt<1>(p, mt, s);
     }
-    if (p.P == 1 && p.res_mode == 0 && p.KK > 1 && rows_form()) {  // a head over whole planes (KK >= 2)
+    if (p.P == 1 && p.res_mode == 0 && p.KK > 1 && form_on(FORM_ROWS)) {  // a head over whole planes (KK >= 2)
         dim3 grid((p.ncols + 31) / 32, (mtiles + 3) / 4);
         hipLaunchKernelGGL((gemm_rows_kernel<true>), grid, dim3(256), 0, s, p, mtiles);
         return "gemm_rows_kernel<true>";

@@ -4,6 +4,7 @@
 // candidate compaction that keeps the bit-exact decode on the host cheap.
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <set>
 #include <string>
@@ -22,6 +23,25 @@ const char *kernel_name(const char *fmt, ...) {
     static std::set<std::string> names;
     std::lock_guard<std::mutex> g(mu);
     return names.insert(buf).first->c_str();
+}
+
+bool form_on(Form f) {
+    static const unsigned mask = [] {
+        static const char *const names[FORM_COUNT] = {"dma", "v4", "valu", "valu_db", "rows", "chain"};
+        unsigned m = ((1u << FORM_COUNT) - 1) & ~(1u << FORM_CHAIN);  // default: every form but chain
+        const char *e = std::getenv("ZARU_HIP_FORMS");
+        for (std::string s = e ? e : ""; !s.empty();) {
+            const size_t comma = s.find(',');
+            const std::string tok = s.substr(0, comma);
+            s = comma == std::string::npos ? "" : s.substr(comma + 1);
+            if (tok.size() < 2 || (tok[0] != '+' && tok[0] != '-')) continue;
+            for (int i = 0; i < FORM_COUNT; i++)
+                if (tok.compare(1, std::string::npos, names[i]) == 0)
+                    m = tok[0] == '+' ? m | (1u << i) : m & ~(1u << i);
+        }
+        return m;
+    }();
+    return (mask >> f) & 1u;
 }
 
 __device__ __forceinline__ const float *plane_ptr(const Plane &p, int n, int c) {

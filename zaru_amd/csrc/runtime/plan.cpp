@@ -788,6 +788,8 @@ int64_t positions(const TRef &r) { return (int64_t)r.H * r.W; }
 // <= 256 positions and <= 128 channels, reading internal tensors only
 bool chain_step_ok(const Step &s) {
     if (s.in.kind != 0 || (s.res_mode && s.in2.kind != 0) || s.out.kind == 1) return false;
+    // chain.hip's epilogue activations are branch-free Relu / PRelu / Clip / none
+    if (s.pre.kind == ACT_SIGMOID || s.post.kind == ACT_SIGMOID || s.dw_act.kind == ACT_SIGMOID) return false;
     if (positions(s.in) > 256 || positions(s.out) > 256 || s.M > 128 || s.K > 128) return false;
     if (s.kind == S_DWPW) return s.kh == 3 && s.kw == 3 && (s.stride == 1 || s.stride == 2);
     if (s.kind == S_GEMM) return s.KK == 1 && s.in.H == s.out.H && s.in.W == s.out.W;
@@ -841,12 +843,14 @@ void Compiler::schedule_sinks() {
 
 // Replace every maximal run (>= 2 steps) of chainable steps whose activations fit in LDS by
 // one S_CHAIN step.  LDS: the entry tensor and every tensor produced and consumed inside the
-// run get regions by liveness (a stride-1 layer may write over the input it consumes last);
-// tensors consumed after the run, and graph outputs, are written to their global homes.
+// run get bordered planes ((H+2) x (W+2) per channel) by liveness; a layer may write over the
+// tensors it consumes last (chain.hip stores after a barrier).  Tensors consumed after the run,
+// and graph outputs, are written to their global homes.
 void Compiler::form_chains() {
     std::vector<Step> &S = P.steps;
+    auto plane = [](const TRef &r) { return (int64_t)(r.H + 2) * (r.W + 2); };
     struct Alloc {
-        std::vector<int> off;  // per op: out region (-1: none)
+        std::vector<int> off;      // per op: out region (-1: none)
         std::map<int, int> where;  // storage id -> LDS offset
         int end = 0, e_off = 0;
         bool ok = false;
@@ -881,36 +885,30 @@ void Compiler::form_chains() {
         auto release = [&](int id) {
             live.erase(std::remove_if(live.begin(), live.end(), [&](const Reg &r) { return r.id == id; }), live.end());
         };
-        const int esz = round4((int64_t)entry.C * positions(entry));
-        A.e_off = 0;
+        const int esz = round4((int64_t)entry.C * plane(entry));
         live.push_back({0, esz, entry.id});
         A.where[entry.id] = 0;
         A.end = esz;
         for (size_t k = i; k <= j; k++) {
             const Step &s = S[k];
-            if (!A.where.count(s.in.id) || (s.res_mode && !A.where.count(s.in2.id))) return A;  // input not in LDS
-            const bool used_later = s.out.kind == 0 && [&] {
+            if (!A.where.count(s.in.id) || (s.res_mode && !A.where.count(s.in2.id))) return A;  // not in LDS
+            bool used_later = false;
+            if (s.out.kind == 0)
                 for (size_t t = k + 1; t <= j; t++)
-                    if (S[t].in.id == s.out.id || (S[t].res_mode && S[t].in2.id == s.out.id)) return true;
-                return false;
-            }();
-            const bool same_p = positions(s.in) == positions(s.out) && s.stride == 1;
-            int prefer = -1;
-            if (same_p && last[s.in.id] == (int)k && (!s.res_mode || s.in2.id == s.in.id)) {
-                prefer = A.where[s.in.id];  // overwrite the consumed input
-                release(s.in.id);
-            }
+                    if (S[t].in.id == s.out.id || (S[t].res_mode && S[t].in2.id == s.out.id)) used_later = true;
+            // inputs read for the last time may be overwritten by this layer's output
+            const int prefer = last[s.in.id] == (int)k ? A.where[s.in.id] : -1;
+            for (auto it = last.begin(); it != last.end(); ++it)
+                if (it->second == (int)k) release(it->first);
             int off = -1;
             if (used_later) {
-                const int sz = round4((int64_t)s.M * positions(s.out));
+                const int sz = round4((int64_t)s.M * plane(s.out));
                 off = place(sz, prefer);
                 live.push_back({off, sz, s.out.id});
                 A.where[s.out.id] = off;
                 A.end = std::max(A.end, off + sz);
             }
             A.off.push_back(off);
-            for (auto it = last.begin(); it != last.end(); ++it)
-                if (it->second == (int)k) release(it->first);
         }
         A.ok = true;
         return A;
@@ -919,21 +917,50 @@ void Compiler::form_chains() {
         const int np = (int)((positions(s.out) + 15) / 16 * 16);
         return np % 32 == 16 ? np : np + 16;
     };
+    // consumer tiling: CHAIN_CONSUMER_WAVES waves as MS groups along M x (waves / MS) along N,
+    // MTW x NTW 16x16 tiles each, from the tilings chain.hip is instantiated for; fewest tiles
+    // per wave
+    struct Tiling {
+        int ms = 0, mtw = 0, ntw = 0;
+    };
+    auto tiling = [](const Step &s) {
+        Tiling best;
+        const int MT = (s.M + 15) / 16, NT = (int)((positions(s.out) + 15) / 16);
+        constexpr int CW = CHAIN_CONSUMER_WAVES;
+        for (int ms : {1, 2, 4, 8})
+            for (const auto &tl : CHAIN_TILINGS) {
+                const int mtw = tl[0], ntw = tl[1];
+                if (ms * mtw < MT || (CW / ms) * ntw < NT) continue;
+                if (!best.ms || mtw * ntw < best.mtw * best.ntw) best = Tiling{ms, mtw, ntw};
+            }
+        return best;
+    };
+    auto mpad_of = [&](const Step &s) {
+        const Tiling t = tiling(s);
+        return std::max(s.Mpad, t.ms * t.mtw * 16);
+    };
+    // per-layer parameters staged in LDS (chain.hip): bias, pre / post PReLU slopes [Mpad],
+    // depthwise channel records [Cin][12]
+    auto param_floats = [&](const Step &s) { return round4(3 * (int64_t)mpad_of(s) + 12 * (int64_t)s.K); };
+    // (chain.hip stages a layer's parameters with 2 per thread: <= 2048 floats)
+    auto step_ok = [&](const Step &s) { return chain_step_ok(s) && tiling(s).ms > 0 && param_floats(s) <= 2048; };
+
     std::vector<Step> out;
     for (size_t i = 0; i < S.size();) {
         const Step &s0 = S[i];
-        const bool entry_ok = chain_step_ok(s0) && positions(s0.in) % 4 == 0 &&
-                              (int64_t)s0.in.C * positions(s0.in) <= 32768;
+        const bool entry_ok = step_ok(s0);
         size_t best_j = i;
         Alloc best;
         if (entry_ok) {
-            for (size_t j = i; j < S.size() && j - i < (size_t)kChainMaxOps && chain_step_ok(S[j]); j++) {
+            for (size_t j = i; j < S.size() && j - i < (size_t)kChainMaxOps && step_ok(S[j]); j++) {
                 Alloc A = layout(i, j, s0.in);
                 if (!A.ok) break;
-                int dmax = 0;
-                for (size_t k = i; k <= j; k++)
+                int dmax = 0, pmax = 0;
+                for (size_t k = i; k <= j; k++) {
                     if (S[k].kind == S_DWPW) dmax = std::max(dmax, d_stride(S[k]));
-                if (A.end + 2 * kChainKC * dmax > kChainLdsFloats) break;
+                    pmax = std::max(pmax, param_floats(S[k]));
+                }
+                if (A.end + 2 * kChainKC * dmax + 2 * pmax > kChainLdsFloats) break;
                 best_j = j;
                 best = A;
             }
@@ -948,17 +975,29 @@ void Compiler::form_chains() {
         c.kind = S_CHAIN;
         c.name = "chain(" + S[i].name + " .. " + S[best_j].name + ")";
         c.in = s0.in;
-        int dmax = 0;
-        for (size_t k = i; k <= best_j; k++)
+        int dmax = 0, pmax = 0;
+        for (size_t k = i; k <= best_j; k++) {
             if (S[k].kind == S_DWPW) dmax = std::max(dmax, d_stride(S[k]));
+            pmax = std::max(pmax, param_floats(S[k]));
+        }
         c.chain_e_off = best.e_off;
         c.chain_d_off = (best.end + 3) / 4 * 4;
         c.chain_d_buf = kChainKC * dmax;
-        c.chain_lds = c.chain_d_off + 2 * c.chain_d_buf;
+        c.chain_p_off = c.chain_d_off + 2 * c.chain_d_buf;
+        c.chain_p_buf = pmax;
+        c.chain_lds = c.chain_p_off + 2 * c.chain_p_buf;
         c.bytes = 4.0 * (double)s0.in.C * positions(s0.in);
         std::vector<ChainOp> ops;
         for (size_t k = i; k <= best_j; k++) {
             const Step &s = S[k];
+            auto ref_of_id = [&](int id) -> TRef {  // geometry of an LDS tensor
+                if (id == s0.in.id) return s0.in;
+                for (size_t t = i; t < k; t++)
+                    if (S[t].out.kind == 0 && S[t].out.id == id) return S[t].out;
+                return TRef{};
+            };
+            const Tiling tl = tiling(s);
+            const int mpad = mpad_of(s), kpad = (s.K + kChainKC - 1) / kChainKC * kChainKC;
             ChainOp o{};
             o.kind = s.kind == S_DWPW ? CHAIN_DWPW : CHAIN_PW;
             o.in_off = best.where[s.in.id];
@@ -966,42 +1005,54 @@ void Compiler::form_chains() {
             o.out_off = best.off[k - i];
             o.Cin = s.K;
             o.Cout = s.M;
-            o.P = (int)positions(s.in);
             o.W = s.in.W;
             o.OP = (int)positions(s.out);
             o.OW = s.out.W;
+            const TRef rin = ref_of_id(s.in.id);
+            o.in_ps = (int)plane(rin);
+            o.in_wp = rin.W + 2;
+            o.out_ps = (int)plane(s.out);
+            o.out_wp = s.out.W + 2;
+            if (s.res_mode) {
+                const TRef rr = ref_of_id(s.in2.id);
+                o.res_ps = (int)plane(rr);
+                o.res_wp = rr.W + 2;
+            }
             o.stride = s.stride;
             o.pad_t = s.pad_t;
             o.pad_l = s.pad_l;
-            o.Mpad = s.Mpad;
-            // wave tiling: 8 waves as MS groups along M x (8 / MS) along N, 16x16 tiles
-            const int MT = (s.M + 15) / 16, NT = (o.OP + 15) / 16;
-            int best_cost = 1 << 30;
-            for (int ms : {1, 2, 4, 8}) {
-                const int mtw = (MT + ms - 1) / ms, ntw = (NT + 8 / ms - 1) / (8 / ms);
-                if (mtw > 4 || ntw > 4 || mtw * ntw >= best_cost) continue;
-                best_cost = mtw * ntw;
-                o.MS = ms;
-                o.MTW = mtw;
-                o.NTW = ntw;
-            }
-            o.NT = NT;
-            if (best_cost == (1 << 30)) return;  // cannot tile: keep the plan unchained
+            o.Mpad = mpad;
+            o.MS = tl.ms;
+            o.MTW = tl.mtw;
+            o.NTW = tl.ntw;
+            o.NT = (o.OP + 15) / 16;
             o.res_mode = s.res_mode;
             o.r_C = s.r_C;
-            o.res_P = s.res_mode ? (int)positions(s.in2) : 0;
-            o.res_W = s.res_mode ? s.in2.W : 0;
-            o.w_off = (int)s.w_off;
-            o.b_off = (int)s.b_off;
+            // zero-padded copies: 1x1 weights [kpad][mpad] (whole 16-row chunks, every wave's
+            // columns), bias and slopes [mpad]
+            std::vector<float> wt((size_t)kpad * mpad, 0.f), bias(mpad, 0.f);
+            for (int kk = 0; kk < s.K; kk++)
+                for (int m = 0; m < s.M; m++) wt[(size_t)kk * mpad + m] = P.weights[s.w_off + (size_t)kk * s.Mpad + m];
+            for (int m = 0; m < s.M; m++) bias[m] = P.weights[s.b_off + m];
+            o.w_off = (int)push_weights(wt);
+            o.b_off = (int)push_weights(bias);
             o.dw_w_off = (int)s.dw_w_off;
             o.dw_b_off = (int)s.dw_b_off;
-            auto act = [](const ActDesc &a) {
-                return ChainAct{a.kind, a.lo, a.hi, (int)a.slope_off};
+            auto act = [&](const ActDesc &a, int n) {
+                ChainAct r{a.kind, a.lo, a.hi, -1};
+                if (a.kind == ACT_PRELU) {
+                    std::vector<float> sl(n, 0.f);
+                    for (int m = 0; m < std::min(n, s.kind == S_DWPW && &a == &s.dw_act ? s.K : s.M); m++)
+                        sl[m] = P.weights[a.slope_off + m];
+                    r.slope_off = (int)push_weights(sl);
+                }
+                return r;
             };
-            o.pre = act(s.pre);
-            o.post = act(s.post);
-            o.dw_act = act(s.dw_act);
+            o.pre = act(s.pre, mpad);
+            o.post = act(s.post, mpad);
+            o.dw_act = act(s.dw_act, s.K);
             o.ds = s.kind == S_DWPW ? d_stride(s) : 0;
+            o.zero_border = 1;
             // a global destination: graph outputs, and internal tensors read after the chain
             bool exported = false;
             if (s.out.kind == 0)
@@ -1014,6 +1065,7 @@ void Compiler::form_chains() {
                 c.chain_outs.push_back(s.out);
                 c.bytes += 4.0 * (double)s.M * positions(s.out);
             }
+            if (o.out_off < 0) o.zero_border = 0;
             ops.push_back(o);
             c.flops += s.flops;
         }
@@ -1072,8 +1124,7 @@ bool Compiler::run(const std::vector<uint32_t> &sel) {
             for (auto &i : M.nodes[ni].in)
                 if (!i.empty()) vals[i].consumers++;
     if (!lower()) return false;
-    const char *fuse = std::getenv("ZARU_HIP_FUSE");  // "0": the unchained plan (verification)
-    if (!(fuse && fuse[0] == '0')) {
+    if (form_on(FORM_CHAIN)) {  // opt-in (ZARU_HIP_FORMS=+chain): see DESIGN.md
         schedule_sinks();
         form_chains();
     }
@@ -1351,11 +1402,14 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook
             c.e_sN = e.sN;
             c.e_sC = e.sC;
             c.e_C = s.in.C;
-            c.e_P = s.in.H * s.in.W;
+            c.e_H = s.in.H;
+            c.e_W = s.in.W;
             c.e_off = s.chain_e_off;
             c.N = b.N;
             c.d_off = s.chain_d_off;
             c.d_buf = s.chain_d_buf;
+            c.p_off = s.chain_p_off;
+            c.p_buf = s.chain_p_buf;
             c.lds_floats = s.chain_lds;
             for (size_t i = 0; i < s.chain_outs.size(); i++) {
                 Resolved o = resolve(s.chain_outs[i], plan, b);

@@ -56,7 +56,7 @@ struct Step {
     int64_t chain_ops_off = -1;
     int chain_nops = 0;
     std::vector<TRef> chain_outs;
-    int chain_e_off = 0, chain_d_off = 0, chain_d_buf = 0, chain_lds = 0;
+    int chain_e_off = 0, chain_d_off = 0, chain_d_buf = 0, chain_p_off = 0, chain_p_buf = 0, chain_lds = 0;
     // algorithmic traffic / work per image (for roofline accounting); bytes_pre: the same
     // step sampling its input from RGBA frames (4 B per input pixel instead of 12)
     double bytes = 0, flops = 0, bytes_pre = 0;

@@ -176,9 +176,10 @@ struct DwPwParams {
 // A run of consecutive low-resolution layers (depthwise 3x3 -> 1x1 BlazeBlocks and plain 1x1
 // convs, <= 256 positions and <= 128 channels per image) executed by ONE workgroup per image
 // with every activation in LDS: the chain reads its entry tensor from HBM once and writes only
-// the tensors consumed outside it (graph outputs, later layers).  The op table is compiled
-// into the session's weight buffer (all fields 32-bit, offsets in floats), so the kernel reads
-// it through the scalar cache; only the binding-dependent pointers travel as kernel arguments.
+// the tensors consumed outside it (graph outputs, later layers).  LDS planes carry a one-cell
+// zero border ((H+2) x (W+2) per channel) so depthwise taps need no bounds checks.  The op table
+// is compiled into the session's weight buffer (all fields 32-bit, offsets in floats), so the
+// kernel reads it through the scalar cache; only binding-dependent pointers are arguments.
 enum ChainOpKind : int { CHAIN_DWPW = 0, CHAIN_PW = 1 };
 
 struct ChainAct {
@@ -189,19 +190,27 @@ struct ChainAct {
 
 struct ChainOp {
     int kind;
-    int in_off, res_off, out_off;   // LDS offsets (floats); res_off / out_off -1: none
-    int Cin, Cout, P, W, OP, OW;    // input channels / positions / width; output positions / width
+    int in_off, res_off, out_off;   // LDS offsets (floats) of bordered planes; -1: none
+    int Cin, Cout, W, OP, OW;       // input channels / width; output positions / width
+    int in_ps, in_wp;               // input plane stride and bordered row width
+    int out_ps, out_wp;             // output plane stride and bordered row width
+    int res_ps, res_wp;             // residual source plane stride and bordered row width
     int stride, pad_t, pad_l;       // depthwise geometry (CHAIN_DWPW)
-    int Mpad, MS, MTW, NTW, NT;     // 1x1 weights [Cin][Mpad]; wave tiling (16x16 MFMA tiles)
-    int res_mode, r_C, res_P, res_W;
+    int Mpad, MS, MTW, NTW, NT;     // 1x1 weights [Kpad16][Mpad]; consumer tiling (16x16 tiles)
+    int res_mode, r_C;
     int w_off, b_off, dw_w_off, dw_b_off;
     ChainAct pre, post, dw_act;
     int gout;                       // global destination index (-1: none)
     int ds;                         // depthwise-output row stride in the D buffers (floats)
+    int zero_border;                // the output region held another tensor: re-zero its border
 };
 static_assert(sizeof(ChainOp) % 4 == 0, "ChainOp is a table of 32-bit words");
 
 constexpr int CHAIN_MAX_OUTS = 8;
+// consumer tilings the kernel is instantiated for: {MTW, NTW} 16x16 tiles per consumer wave
+constexpr int CHAIN_CONSUMER_WAVES = 8;
+constexpr int CHAIN_TILINGS[][2] = {{1, 1}, {1, 2}, {1, 3}, {1, 9}, {2, 1}, {2, 2}, {3, 1}, {3, 2},
+                                    {3, 4}, {4, 1}, {4, 2}};
 
 struct ChainOut {  // element (n, c, q) at p + n*sN + c*sC + q*sP
     float *p;
@@ -213,12 +222,23 @@ struct ChainParams {
     int ops_off, nops;              // op table at weights + ops_off (floats)
     const float *entry;             // entry tensor, CNHW: (n, c, p) at entry + n*e_sN + c*e_sC + p
     int64_t e_sN, e_sC;
-    int e_C, e_P, e_off;            // channels, positions, LDS offset
+    int e_C, e_H, e_W, e_off;       // geometry and LDS offset (bordered planes)
     int N;
     int d_off, d_buf;               // D buffers: two of d_buf floats at LDS offset d_off
+    int p_off, p_buf;               // per-layer parameters staged in LDS: two of p_buf floats
     int lds_floats;
     ChainOut gout[CHAIN_MAX_OUTS];
 };
+
+// Kernel forms the launchers and the plan compiler choose between.  Every form computes the same
+// arithmetic in the same order, so switching one changes no output bit (tests/test_gpu_forms.py).
+// ZARU_HIP_FORMS, read once per process, switches forms off ("-dma,-v4") or the opt-in chain form
+// on ("+chain"), for verification and A/B runs.
+//   dma: LDS-DMA staged MFMA dwpw (dwpw_dma_kernel)   v4: windowed depthwise taps (dwpw_kernel)
+//   valu: VALU dwpw for few-channel high-resolution layers   valu_db: its double-buffered staging
+//   rows: image-row head GEMM (gemm_rows_kernel)   chain: low-resolution layer runs (chain.hip)
+enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_CHAIN, FORM_COUNT };
+bool form_on(Form f);
 
 bool stem_supported(int cin, int k, int stride, int cout);
 bool dwpw_supported(int k, int stride);
