@@ -38,8 +38,9 @@ SWITCHES = {
     "no_dma": "-dma",
     "no_v4": "-v4,-dma",
     "no_rows": "-rows",
+    "no_vres": "-vres",
     "chain": "+chain",  # low-resolution layer runs in one launch per image (chain.hip)
-    "all_off": "-dma,-v4,-valu,-valu_db,-rows",
+    "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres",
 }
 
 

@@ -19,6 +19,7 @@
 namespace zr {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------ stem
 constexpr int STH = 8, STW = 32;  // output tile: 8 rows x 32 columns, one pixel per thread
@@ -539,6 +540,179 @@ __global__ __launch_bounds__(256) void dwpw_valu_kernel(const DwPwParams P, int 
         if (m < G.M) G.out[ob + (uint32_t)m * (uint32_t)G.o_sC] = v[m];
 }
 
+// The BlazeBlock case of the DB VALU form (form "vres"): the residual is the block input, i.e.
+// the depthwise input the chunks already stage -- at stride 1 its value at a position is the
+// centre tap (pad, pad), at stride 2 its 2x2 max-pool is the max of taps (pad..pad+1)^2 (TF-style
+// pads, even planes).  So the residual is captured from the taps in registers while the
+// depthwise runs, and the epilogue has no loads left: a tile's lifetime loses one HBM round trip
+// and the launch a third of its reads.  Needs Cin <= CO (each input channel's residual lands in
+// its own register) and no depthwise activation; the chunk loop is unrolled so every register
+// index is static.  Same arithmetic, same order as dwpw_valu_kernel.
+// WL: the layer's weights are staged in LDS (see below) -- for launches of few tiles, where each
+// CU's scalar cache is cold for every channel; otherwise they come through the scalar cache.
+template <int K, int S, int CO, int VF, int RES, bool WL>
+__global__ __launch_bounds__(256) void dwpw_vres_kernel(const DwPwParams P, int tpi, int ntiles, int bufsz, int lw) {
+    extern __shared__ __attribute__((aligned(16))) float sIn[];  // two buffers of [VF * rows][lw]
+    constexpr int NCH = (CO + VF - 1) / VF, PL = DwPad<K, S>::L, DMAX = 6, VT = VTQ, NW = 4;
+    const GemmParams &G = P.g;
+    const int cpx = gridDim.x >> 3;  // gridDim.x is a multiple of 8
+    const int tile = (blockIdx.x & 7) * cpx + (blockIdx.x >> 3);
+    if (tile >= ntiles) return;  // whole workgroup, before any barrier
+    const int tid = threadIdx.x;
+    const int n = tile / tpi, q0 = (tile - n * tpi) * VT;
+    const int Pq = G.P, H = P.in.H, W = P.in.W, Cin = G.K, OW = P.OW, r_C = G.r_C;
+    const int oy_a = q0 / OW, oy_b = min(q0 + VT - 1, Pq - 1) / OW;
+    const int iy_a = oy_a * S - P.pad_t;
+    const int R = (oy_b - oy_a) * S + K;
+    const int q = min(q0 + tid, Pq - 1);
+    const int oy = q / OW, ox = q - oy * OW;
+    const int lb = (oy * S - P.pad_t - iy_a) * lw + 4 - P.pad_l + ox * S;  // tap (0, 0)
+    const uint32_t nbase = (uint32_t)n * (uint32_t)P.in.sN;
+    const int srow = (W >> 2) + 2;
+    const float inv_srow = 1.f / (float)srow, inv_R = 1.f / (float)R;
+
+    f32x2 acc[CO / 2];
+    float rv[CO];
+#pragma unroll
+    for (int i = 0; i < CO / 2; ++i) acc[i] = (f32x2)(0.f);
+#pragma unroll
+    for (int m = 0; m < CO; ++m) rv[m] = 0.f;
+
+    const int total = VF * R * srow;
+    const int nwi = (total + 63) >> 6, lane = tid & 63, wave = tid >> 6;
+    const bool pre_off = nwi <= NW * DMAX;
+    int goff[DMAX], gch[DMAX];
+#pragma unroll
+    for (int m = 0; m < DMAX; ++m) {
+        const int sl = (wave + NW * m) * 64 + lane;
+        const int cr = qdiv(sl, srow, inv_srow), sx = sl - cr * srow;
+        const int c = qdiv(cr, R, inv_R), r = cr - c * R;
+        const int iy = iy_a + r, xv = sx - 1;
+        const bool ok = sl < total && iy >= 0 && iy < H && xv >= 0 && 4 * xv < W;
+        goff[m] = ok ? (int)((uint32_t)c * (uint32_t)P.in.sC + nbase + (uint32_t)(iy * W + 4 * xv)) : -1;
+        gch[m] = c;
+    }
+    auto stage_dma = [&](int kc, float *dst) {
+        if (pre_off) {
+            const float *base = P.in.p + (size_t)(uint32_t)kc * (uint32_t)P.in.sC;
+            const int cl = Cin - kc;
+#pragma unroll
+            for (int m = 0; m < DMAX; ++m) {
+                const int wi = wave + NW * m;
+                if (wi < nwi) {
+                    const bool ok = goff[m] >= 0 && gch[m] < cl;
+                    const float *src = ok ? base + (uint32_t)goff[m] : (const float *)&zr_zero4;
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                                     (__attribute__((address_space(3))) void *)(dst + wi * 256), 16, 0, 0);
+                }
+            }
+            return;
+        }
+        for (int wi = wave; wi < nwi; wi += NW) {
+            const int sl = wi * 64 + lane;
+            const int cr = qdiv(sl, srow, inv_srow), sx = sl - cr * srow;
+            const int c = qdiv(cr, R, inv_R), r = cr - c * R;
+            const int iy = iy_a + r, ch = kc + c, xv = sx - 1;
+            const bool ok = sl < total && iy >= 0 && iy < H && ch < Cin && xv >= 0 && 4 * xv < W;
+            const float *src = ok ? P.in.p + (size_t)(uint32_t)ch * (uint32_t)P.in.sC + nbase + (uint32_t)(iy * W + 4 * xv)
+                                  : (const float *)&zr_zero4;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                             (__attribute__((address_space(3))) void *)(dst + wi * 256), 16, 0, 0);
+        }
+    };
+    // the layer's weights into LDS once, behind the two stage buffers: 1x1 [Cin][CO], depthwise
+    // records [Cin][RS] (K*K weights, bias, zeros).  The loop then reads only LDS (in-order
+    // returns, so the compiler can run loads ahead under lgkmcnt(N)); scalar loads there would
+    // share lgkmcnt and, returning out of order, force lgkmcnt(0) per channel.
+    constexpr int RS = (K * K + 1 + 3) / 4 * 4;
+    float *sW = sIn + 2 * bufsz, *sD = sW + Cin * CO;
+    if constexpr (WL) {
+    for (int i = tid; i < Cin * CO; i += 64 * NW) {
+        const int k = i / CO, m = i - k * CO;
+        sW[i] = G.wt[(size_t)k * G.Mpad + m];
+    }
+    for (int i = tid; i < Cin * RS; i += 64 * NW) {
+        const int c = i / RS, e = i - c * RS;
+        sD[i] = e < K * K ? P.dw_w[c * K * K + e] : e == K * K ? P.dw_b[c] : 0.f;
+    }
+    }
+    stage_dma(0, sIn);
+
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+        const int kc = j * VF;
+        if (kc >= Cin) break;
+        const float *buf = sIn + (j & 1) * bufsz;
+        // every wave's DMA of chunk j has landed (explicit: the barrier alone does not promise
+        // it), then chunk j - 1's readers are done with the other buffer
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (kc + VF < Cin) stage_dma(kc + VF, sIn + ((j + 1) & 1) * bufsz);
+        // one channel: depthwise from the staged taps, residual capture, 1x1 accumulation
+        auto chan = [&](int c, int ch) {
+            const float *t0 = buf + c * R * lw + lb;
+            float t[K * K], wk[RS];
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx) t[ky * K + kx] = t0[ky * lw + kx];
+            if constexpr (WL) {
+#pragma unroll
+                for (int e = 0; e < RS; e += 4) *(f32x4 *)(wk + e) = *(const f32x4 *)(sD + ch * RS + e);  // broadcast
+            } else {
+#pragma unroll
+                for (int e = 0; e < K * K; ++e) wk[e] = ldc(P.dw_w, ch * K * K + e);
+                wk[K * K] = ldc(P.dw_b, ch);
+            }
+            float d = wk[K * K];
+#pragma unroll
+            for (int k = 0; k < K * K; ++k) d = __builtin_fmaf(wk[k], t[k], d);
+            float r = t[PL * K + PL];
+            if constexpr (RES == 2)
+                r = fmaxf(fmaxf(r, t[PL * K + PL + 1]), fmaxf(t[(PL + 1) * K + PL], t[(PL + 1) * K + PL + 1]));
+            rv[ch] = ch < r_C ? r : 0.f;
+            if constexpr (WL) {
+                const f32x4 *w4 = (const f32x4 *)(sW + ch * CO);  // broadcast
+#pragma unroll
+                for (int i = 0; i < CO / 4; ++i) {
+                    const f32x4 w = w4[i];
+                    acc[2 * i] = __builtin_elementwise_fma(f32x2{w.x, w.y}, (f32x2)(d), acc[2 * i]);
+                    acc[2 * i + 1] = __builtin_elementwise_fma(f32x2{w.z, w.w}, (f32x2)(d), acc[2 * i + 1]);
+                }
+            } else {
+                const __attribute__((address_space(4))) f32x2 *w2 =
+                    (const __attribute__((address_space(4))) f32x2 *)(G.wt + (size_t)ch * G.Mpad);  // [Kpad][Mpad]
+#pragma unroll
+                for (int i = 0; i < CO / 2; ++i) acc[i] = __builtin_elementwise_fma(w2[i], (f32x2)(d), acc[i]);
+            }
+        };
+#pragma unroll
+        for (int c = 0; c < VF; ++c) {
+            // (a per-channel exit measured faster than straight-line whole chunks: the scheduler
+            // then keeps fewer loads in flight but the occupancy and the scalar cache hold up)
+            if (kc + c >= Cin || kc + c >= CO) break;
+            chan(c, kc + c);
+        }
+    }
+
+    if (q0 + tid >= Pq) return;
+    float v[CO];
+#pragma unroll
+    for (int i = 0; i < CO / 2; ++i) {
+        v[2 * i] = acc[i].x + G.bias[2 * i];
+        v[2 * i + 1] = acc[i].y + G.bias[2 * i + 1];
+    }
+    auto chan = [](int m) { return m; };
+    apply_act_n<CO>(G.pre, v, chan);
+#pragma unroll
+    for (int m = 0; m < CO; ++m) v[m] += rv[m];
+    apply_act_n<CO>(G.post, v, chan);
+    const uint32_t ob = (uint32_t)n * (uint32_t)G.o_sN + (uint32_t)q * (uint32_t)G.o_sP;
+#pragma unroll
+    for (int m = 0; m < CO; ++m)
+        if (m < G.M) G.out[ob + (uint32_t)m * (uint32_t)G.o_sC] = v[m];
+}
+
 // LDS-DMA form of the MFMA dwpw for the stride-1 low-resolution layers (24^2 ... 6^2 planes
 // with 64-256 channels), whose register-staged form waits on memory most of the time.  Per
 // chunk of DFKC input channels one buffer receives, by global_load_lds_dwordx4 (no VGPRs, no
@@ -762,6 +936,52 @@ const char *dwpw_layout(const DwPwParams &p, const DwPwLayout &l, hipStream_t s)
     }
 }
 
+// The vres form's case (see dwpw_vres_kernel): 1 = residual is the centre tap, 2 = its 2x2
+// max-pool from the taps, 0 = not applicable.
+static int vres_mode(const DwPwParams &p, int S, int CO) {
+    const GemmParams &g = p.g;
+    if (!form_on(FORM_VRES) || g.res_mode == 0 || g.r != p.in.p || g.r_sN != p.in.sN || g.r_sC != p.in.sC ||
+        g.K > CO || g.r_C > g.K || p.dw_act.kind != ACT_NONE)
+        return 0;
+    const int pl = S == 1 ? p.k / 2 : p.k / 2 - 1;
+    if (p.pad_t != pl || p.pad_l != pl || pl < 0) return 0;
+    const int OH = g.P / p.OW;
+    if (g.res_mode == 1 && S == 1 && p.OW == p.in.W && OH == p.in.H) return 1;
+    if (g.res_mode == 2 && S == 2 && g.r_W == p.in.W && p.in.H % 2 == 0 && p.in.W % 2 == 0 &&
+        2 * p.OW == p.in.W && 2 * OH == p.in.H && pl + 1 < p.k)
+        return 2;
+    return 0;
+}
+
+template <int K, int S, int CO>
+const char *dwpw_vres_go(const DwPwParams &p, hipStream_t s) {
+    const int P = p.g.P, N = p.g.ncols / P, vt = VTQ;
+    const int tpi = (P + vt - 1) / vt, ntiles = tpi * N;
+    int rmax = 0;
+    for (int t = 0; t < tpi; t++) {
+        const int q0 = t * vt, a = q0 / p.OW, b = std::min(q0 + vt - 1, P - 1) / p.OW;
+        rmax = std::max(rmax, (b - a) * S + K);
+    }
+    const int lw = p.in.W + 8;
+    auto buf_of = [&](int vf) { return (vf * rmax * lw + 255) / 256 * 256; };  // whole 1 KiB DMA rows
+    // 8-channel chunks for 32 channels where two buffers fit 64 KiB (as measured for
+    // dwpw_valu_kernel), else 4
+    const bool vf8 = 2 * sizeof(float) * (size_t)buf_of(VFKC) <= 64 * 1024 && CO == 32;
+    const int vf = vf8 ? VFKC : 4, bufsz = buf_of(vf);
+    dim3 grid((ntiles + 7) / 8 * 8);
+    constexpr int mode = S;  // vres_mode: centre tap at stride 1, 2x2 pool at stride 2
+    const bool wl = ntiles < 2048;  // measured: LDS weights win below ~8 tiles per CU, lose above
+    const size_t lds = sizeof(float) * (2 * (size_t)bufsz + (wl ? (size_t)p.g.K * (CO + (K * K + 4) / 4 * 4) : 0));
+    if (wl) {
+        if (vf8) hipLaunchKernelGGL((dwpw_vres_kernel<K, S, CO, VFKC, mode, true>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
+        else hipLaunchKernelGGL((dwpw_vres_kernel<K, S, CO, 4, mode, true>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
+    } else {
+        if (vf8) hipLaunchKernelGGL((dwpw_vres_kernel<K, S, CO, VFKC, mode, false>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
+        else hipLaunchKernelGGL((dwpw_vres_kernel<K, S, CO, 4, mode, false>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
+    }
+    return kernel_name("dwpw_vres_kernel<%d,%d,%d,%d,%d,%s>", K, S, CO, vf, mode, wl ? "true" : "false");
+}
+
 template <int K, int S, int CO>
 const char *dwpw_valu_go(const DwPwParams &p, hipStream_t s) {
     const int P = p.g.P, tpi = (P + VTQ - 1) / VTQ, ntiles = tpi * (p.g.ncols / P);
@@ -774,15 +994,18 @@ const char *dwpw_valu_go(const DwPwParams &p, hipStream_t s) {
     // Double-buffered LDS-DMA staging (form valu_db).  Measured per CO: 32 channels: 8-channel
     // chunks while two buffers fit 64 KiB (the 131 VGPRs hold a CU to 3 workgroups anyway), else
     // 4-channel chunks; 16 channels: 4-channel chunks, so two buffers cost no more LDS (and
-    // occupancy) than one 8-channel buffer; 48 channels: only at stride 2 (slower at stride 1).
+    // occupancy) than one 8-channel buffer; 48 channels: at stride 2, and at stride 1 in the
+    // vres form (the residual-loading form is slower there).
     auto buf_of = [&](int vf) { return (vf * rmax * lw + 255) / 256 * 256; };  // whole 1 KiB DMA rows
     const bool fit8 = 2 * sizeof(float) * (size_t)buf_of(VFKC) <= 64 * 1024;
-    const bool db = form_on(FORM_VALU_DB) && (CO == 16 || CO == 32 || (CO == 48 && S == 2)) &&
+    const int vres = vres_mode(p, S, CO);
+    const bool db = form_on(FORM_VALU_DB) && (CO == 16 || CO == 32 || (CO == 48 && (S == 2 || vres))) &&
                     2 * sizeof(float) * (size_t)buf_of(4) <= 64 * 1024;
     const bool small = db && !(CO == 32 && fit8);
     const int vf = small ? 4 : VFKC;
     const int bufsz = buf_of(vf);
     dim3 grid((ntiles + 7) / 8 * 8);
+    if (db && vres) return dwpw_vres_go<K, S, CO>(p, s);
     if (db) {
         const size_t lds = 2 * sizeof(float) * (size_t)bufsz;
         if (small)

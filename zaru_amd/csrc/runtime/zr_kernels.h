@@ -237,7 +237,8 @@ struct ChainParams {
 //   dma: LDS-DMA staged MFMA dwpw (dwpw_dma_kernel)   v4: windowed depthwise taps (dwpw_kernel)
 //   valu: VALU dwpw for few-channel high-resolution layers   valu_db: its double-buffered staging
 //   rows: image-row head GEMM (gemm_rows_kernel)   chain: low-resolution layer runs (chain.hip)
-enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_CHAIN, FORM_COUNT };
+//   vres: VALU dwpw taking the block's residual from the staged depthwise taps
+enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_CHAIN, FORM_VRES, FORM_COUNT };
 bool form_on(Form f);
 
 bool stem_supported(int cin, int k, int stride, int cout);
