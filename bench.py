@@ -53,12 +53,22 @@ SURVEY_BYTES = {"face_detection_short_range": 11.02e6, "face_landmark": 16.56e6,
                 "palm_detection_lite": 51.58e6, "hand_landmark_lite": 37.20e6}
 SURVEY_FLOPS = {"face_detection_short_range": 61.52e6, "face_landmark": 69.96e6,
                 "palm_detection_lite": 566.34e6, "hand_landmark_lite": 291.21e6}
+# SURVEY §8f-1 networks have no §8d figure: their compiled plans' own per-image bytes at fused
+# kernel boundaries and FLOPs (zr_plan_describe; for the four §8d networks these plan bytes
+# are 0.64-0.65x the §8d layer-boundary model, so this is the stricter denominator)
+SURVEY_BYTES.update({"face_detection_full_range": 30.08e6, "face_landmarks_detector": 39.93e6})
+SURVEY_FLOPS.update({"face_detection_full_range": 211.34e6, "face_landmarks_detector": 225.73e6})
 
 WORKLOADS = {
     # kind: detector, landmark net, det input, landmark input, ROIs per frame, seed (§8d)
     "face": ("face_detection_short_range", "face_landmark", 128, 192, 1, 3),
     "hand": ("palm_detection_lite", "hand_landmark_lite", 192, 224, 4, 4),
+    # BlazeFace full range -> FaceMesh V2 (478 points) on config 3's frames
+    "face_next": ("face_detection_full_range", "face_landmarks_detector", 192, 256, 1, 3),
 }
+# pipeline kind and network overrides of each workload (DetectTrackPipeline arguments)
+PIPELINE = {"face": ("face", "", ""), "hand": ("hand", "", ""),
+            "face_next": ("face", "face_full", "facemesh_v2")}
 
 
 def parse():
@@ -67,7 +77,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1024, help="frames per step per GPU")
-    ap.add_argument("--workload", choices=["face", "hand", "both"], default="face")
+    ap.add_argument("--workload", choices=["face", "hand", "both", "face_next"], default="face")
     ap.add_argument("--threads", type=int, default=16, help="host decode/map threads per rank")
     ap.add_argument("--sub-batches", type=int, default=3)
     ap.add_argument("--streams", choices=["multi", "single"], default="multi")
@@ -79,6 +89,10 @@ def parse():
     ap.add_argument("--no-hand", action="store_true", help="skip the config-4 line at N = 1")
     ap.add_argument("--hand-steps", type=int, default=30)
     ap.add_argument("--hand-batch", type=int, default=256)
+    ap.add_argument("--no-next", action="store_true",
+                    help="skip the SURVEY §8f-1 line (full range + FaceMesh V2) at N = 1")
+    ap.add_argument("--next-steps", type=int, default=30)
+    ap.add_argument("--next-batch", type=int, default=512)
     return ap.parse_args()
 
 
@@ -172,7 +186,7 @@ def measure_traffic(args, kind):
     if not shutil.which("rocprofv3"):
         return None
     child = [sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
-             "--no-cpu-baseline", "--no-profile", "--no-traffic", "--no-hand",
+             "--no-cpu-baseline", "--no-profile", "--no-traffic", "--no-hand", "--no-next",
              "--batch", str(args.batch), "--workload", kind,
              "--sub-batches", str(args.sub_batches), "--streams", args.streams]
     kib, launches = {}, {}
@@ -292,23 +306,26 @@ class Workload:
         det, lm, din, lin, rois, seed = WORKLOADS[kind]
         self.kind, self.batch, self.det, self.lm = kind, batch, det, lm
         rng = np.random.default_rng(seed + 1000 * rank)
+        base, dnet, lnet = PIPELINE[kind]
         if shared is None:
-            self.fs = FrameSet(rng, batch, patch=load_patch() if kind == "face" else None)
+            self.fs = FrameSet(rng, batch, patch=load_patch() if base == "face" else None)
             self.frames = self.fs.to_device(f"cuda:{device}")
         else:  # config 5: the other pipeline's frames (the same camera streams)
             self.fs, self.frames = shared.fs, shared.frames
-        forced = forced_rois(rng, batch, kind)
+        forced = forced_rois(rng, batch, base)
         fp, fb = self.frames.data_ptr(), 1080 * 1920 * 4
         self.flist = [(fp + i * fb, 1920, 1080, 1920 * 4) for i in range(batch)]
         self.forced = forced
-        self.args = (kind, device, threads, rois, sub_batches)
-        self.pipe = H.DetectTrackPipeline(kind, device, threads, rois, sub_batches, multi_stream)
+        self.args = (base, device, threads, rois, sub_batches)
+        self.nets = {"detector": dnet, "landmarker": lnet}
+        self.pipe = H.DetectTrackPipeline(base, device, threads, rois, sub_batches, multi_stream,
+                                          **self.nets)
         self.pipe.set_frames(self.flist, forced)
 
     def profiled(self, H, steps):
         """Per-kernel HIP-event times with the sub-batches on one stream (uncontended)."""
         kind, device, threads, rois, sub_batches = self.args
-        p = H.DetectTrackPipeline(kind, device, threads, rois, sub_batches, False)
+        p = H.DetectTrackPipeline(kind, device, threads, rois, sub_batches, False, **self.nets)
         p.set_frames(self.flist, self.forced)
         p.run_frames_repeated(2)
         p.profile_read()
@@ -347,14 +364,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    primary = "hand" if args.workload == "hand" else "face"
+    primary = args.workload if args.workload in ("hand", "face_next") else "face"
     # child processes first, while this one has not touched the GPU: PMC traffic passes,
     # then the CPU baseline (its workers would otherwise compete with the pipeline's threads)
     traffic = None
     if world == 1 and not args.no_traffic and not args.no_profile:
         traffic = measure_traffic(args, primary)
     cpu = None
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and primary in ("face", "hand"):
         cpu = cpu_baseline(primary, args.cpu_baseline_seconds, args.batch, WORKLOADS[primary][5])
 
     import torch
@@ -418,10 +435,11 @@ def main():
     flops_frame = SURVEY_FLOPS[wl.det] + rois_per_frame * SURVEY_FLOPS[wl.lm]
     pipe_gbs = frames_per_s_gpu * bytes_frame / 1e9
     out = {
-        "metric": METRIC if wl.kind == "face" else
-        "end-to-end hand landmark ROIs/sec (palm detect + 21-pt hand landmarks, 4 ROIs/frame)",
-        "value": round(tracked / elapsed, 1) if wl.kind == "face" else round(rois / elapsed, 1),
-        "unit": "faces/s" if wl.kind == "face" else "hand ROIs/s",
+        "metric": {"face": METRIC, "face_next": NEXT_METRIC,
+                   "hand": "end-to-end hand landmark ROIs/sec (palm detect + 21-pt hand landmarks, "
+                           "4 ROIs/frame)"}[wl.kind],
+        "value": round(rois / elapsed, 1) if wl.kind == "hand" else round(tracked / elapsed, 1),
+        "unit": "hand ROIs/s" if wl.kind == "hand" else "faces/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -431,10 +449,11 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic: seeded uniform-noise 1920x1080 RGBA8 frames"
-                + (" + one 576x576 face patch each (reference test image, upscaled)" if wl.kind == "face" else "")
+                + (" + one 576x576 face patch each (reference test image, upscaled)" if wl.kind != "hand" else "")
                 + "; forced seeded ROI when no detection; ONNX weights from the reference",
         "config": {"workload": {"face": "config 3: BlazeFace -> FaceMesh V1 face pipeline",
-                                "hand": "config 4: palm lite + hand landmark lite, 4 ROIs/frame"}[wl.kind]
+                                "hand": "config 4: palm lite + hand landmark lite, 4 ROIs/frame",
+                                "face_next": NEXT_WORKLOAD}[wl.kind]
                    + (" + config 4 hand pipeline concurrently on its own streams (config 5)" if len(wls) > 1 else ""),
                    "frames_per_gpu_per_step": args.batch, "frame": "1920x1080 RGBA8",
                    "sub_batches": args.sub_batches, "streams": args.streams,
@@ -468,10 +487,48 @@ def main():
         out["kernels"] = sorted(kernels, key=lambda k: -k["ms"])
     if world == 1 and args.workload == "face" and not args.no_hand:
         out["hand"] = hand_line(H, args, device)
+    if world == 1 and args.workload == "face" and not args.no_next:
+        out["face_next"] = next_line(H, args, device)
     out["cpu_baseline"] = cpu
     print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+
+
+NEXT_METRIC = "end-to-end faces/sec (full-range detect + 478-pt FaceMesh V2), 1080p synthetic"
+NEXT_WORKLOAD = "SURVEY 8f-1: BlazeFace full range -> FaceMesh V2 face pipeline (config 3 frames)"
+
+
+def next_line(H, args, device):
+    """SURVEY §8f-1 on the same GPU after the face line: BlazeFace full range (192^2, 2304
+    anchors) -> FaceMesh V2 (256^2, 478 points) over config 3's frame generator."""
+    import torch
+    w = Workload(H, "face_next", device, args.next_batch, 0, args.threads, args.sub_batches,
+                 args.streams == "multi")
+    run_steps([w], 5, None, 0, 1, None)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    t = run_steps([w], args.next_steps, None, 0, 1, None)[0]
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    fps = t["frames"] / elapsed
+    bpf = SURVEY_BYTES[w.det] + 16.0 * 192 * 192 + (t["rois"] / t["frames"]) * (
+        SURVEY_BYTES[w.lm] + 16.0 * 256 * 256)
+    out = {"metric": NEXT_METRIC, "value": round(t["tracked"] / elapsed, 1), "unit": "faces/s",
+           "workload": NEXT_WORKLOAD, "frames_per_s": round(fps, 1),
+           "tracked_per_step": round(t["tracked"] / args.next_steps, 2),
+           "ms_per_step": round(1e3 * elapsed / args.next_steps, 3), "steps": args.next_steps,
+           "frames_per_step": args.next_batch,
+           "pipeline_roofline": {"model": "plan fused-boundary bytes per image (zr_plan_describe)",
+                                 "bytes_per_frame": round(bpf),
+                                 "achieved_GBs": round(fps * bpf / 1e9, 1),
+                                 "frac": round(fps * bpf / 1e9 / HBM_PEAK_GBS, 4)}}
+    if not args.no_profile:
+        kernels, _ = w.profiled(H, 5)
+        out["roofline"] = roofline_of(kernels, None)
+        out["kernels"] = sorted(kernels, key=lambda k: -k["ms"])[:8]
+    del w
+    return out
 
 
 def hand_line(H, args, device):

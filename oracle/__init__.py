@@ -138,6 +138,8 @@ def _lib():
     L.zo_net_run_f64out.restype = C.c_int
     L.zo_net_run_f64out.argtypes = [P, P, P]
     L.zo_net_error.restype = C.c_char_p
+    L.zo_net_tensor.restype = sz
+    L.zo_net_tensor.argtypes = [P, C.c_char_p, P, sz, P, P]
     _LIB = L
     return L
 
@@ -222,9 +224,11 @@ def preproc(img: np.ndarray, view: RRect, ow: int, oh: int, lo: float, hi: float
 
 
 # ---------------------------------------------------------------- decode / NMS
-FACE, PALM = 0, 1
-FACE_LAYERS = [(2, 16, 16), (6, 8, 8)]
-PALM_LAYERS = [(2, 24, 24), (6, 12, 12)]
+FACE, PALM, FACE_FULL = 0, 1, 2
+FACE_LAYERS = [(2, 16, 16), (6, 8, 8)]        # face/detection.rs:53
+PALM_LAYERS = [(2, 24, 24), (6, 12, 12)]      # hand/detection.rs:117
+FACE_FULL_LAYERS = [(1, 48, 48)]              # face/detection.rs:86-88
+LAYERS = {FACE: FACE_LAYERS, PALM: PALM_LAYERS, FACE_FULL: FACE_FULL_LAYERS}
 
 
 def anchors(layers) -> np.ndarray:
@@ -236,8 +240,7 @@ def anchors(layers) -> np.ndarray:
 
 
 def extract(kind, boxes, confs, in_w, in_h, thresh=0.5):
-    layers = FACE_LAYERS if kind == FACE else PALM_LAYERS
-    an = anchors(layers)
+    an = anchors(LAYERS[kind])
     boxes = np.ascontiguousarray(boxes, np.float32)
     confs = np.ascontiguousarray(confs, np.float32).reshape(-1)
     out = (Det * len(an))()
@@ -277,14 +280,15 @@ def tracker_update(pos, view_rect: RRect, roi_rad, est_angle, padding):
     return p, upd, nxt
 
 
-FACEMESH, HAND = 0, 1
+FACEMESH, HAND, FACEMESH_V2 = 0, 1, 2
 
 
 def landmark_angle(kind, pos) -> float:
     """Estimate::angle_radians of view-local landmarks (FACEMESH: mediapipe.rs:146-160,
     HAND: hand/landmark.rs:68-78)."""
     p = np.ascontiguousarray(pos, np.float32)
-    return _lib().zo_landmark_angle(kind, _ptr(p))
+    # FaceMesh V2 uses V1's eye-corner indices (mediapipe.rs:407-421)
+    return _lib().zo_landmark_angle(HAND if kind == HAND else FACEMESH, _ptr(p))
 
 
 def landmark_confidence(kind, outs) -> float:
@@ -292,7 +296,7 @@ def landmark_confidence(kind, outs) -> float:
     sigmoid(out1) (mediapipe.rs:60), hand presence = out1 (sigmoid inside the graph,
     hand/landmark.rs:309)."""
     v = float(np.asarray(outs[1], np.float32).reshape(-1)[0])
-    return sigmoid(v) if kind == FACEMESH else v
+    return v if kind == HAND else sigmoid(v)  # V2: face_flag as V1 (mediapipe.rs:100)
 
 
 # ---------------------------------------------------------------- networks
@@ -329,3 +333,14 @@ class Net:
         if fn(self._h, _ptr(x), ptrs):
             raise RuntimeError(_lib().zo_net_error().decode())
         return outs
+
+    def tensor(self, name: str) -> np.ndarray:
+        """Any intermediate tensor of the last run (f64 nets; layer bisection)."""
+        shape = np.zeros(6, np.int64)
+        rank = C.c_size_t(0)
+        n = _lib().zo_net_tensor(self._h, name.encode(), None, 0, _ptr(shape), C.byref(rank))
+        if not n:
+            raise KeyError(name)
+        out = np.empty(n, np.float64)
+        _lib().zo_net_tensor(self._h, name.encode(), _ptr(out), n, None, None)
+        return out.reshape(tuple(int(v) for v in shape[:rank.value]))

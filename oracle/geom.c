@@ -245,11 +245,13 @@ size_t zo_anchors(const uint32_t *layers, size_t nlayers, float *out_xy) {
     return n;
 }
 
-/* face/detection.rs:96-157 (kind 0) and hand/detection.rs:108-179 (kind 1) */
+/* face/detection.rs:96-157 (kind 0 short range, kind 2 full range: the same
+ * extract_outputs over different anchors) and hand/detection.rs:108-179 (kind 1) */
 size_t zo_extract(int kind, const float *boxes, const float *confs, size_t nanchors,
                   const float *anchors_xy, uint32_t in_w, uint32_t in_h, float thresh,
                   zo_det *out, size_t cap) {
-    size_t np = kind == 0 ? 16 : 18, nkp = kind == 0 ? 6 : 7, n = 0;
+    const int face = kind != 1;
+    size_t np = face ? 16 : 18, nkp = face ? 6 : 7, n = 0;
     float isx = (float)in_w, isy = (float)in_h;
     for (size_t i = 0; i < nanchors; i++) {
         float conf = zo_sigmoid(confs[i]);
@@ -268,7 +270,7 @@ size_t zo_extract(int kind, const float *boxes, const float *confs, size_t nanch
             d->kp[k][0] = b[4 + 2 * k] + cx * isx;
             d->kp[k][1] = b[5 + 2 * k] + cy * isy;
         }
-        if (kind == 0) {
+        if (face) {
             float dx = d->kp[1][0] - d->kp[0][0], dy = d->kp[1][1] - d->kp[0][1];
             d->angle = zo_signed_angle_to(dx, dy, 1.0f, 0.0f);
         } else {
@@ -392,10 +394,13 @@ size_t zo_detect_post(int kind, const float *boxes, const float *confs, size_t n
                       float thresh, float iou, zo_det *out, size_t cap) {
     uint32_t face_layers[] = {2, 16, 16, 6, 8, 8};   /* face/detection.rs:53 */
     uint32_t palm_layers[] = {2, 24, 24, 6, 12, 12}; /* hand/detection.rs:117 */
-    size_t na = zo_anchors(kind == 0 ? face_layers : palm_layers, 2, NULL);
+    uint32_t full_layers[] = {1, 48, 48};            /* face/detection.rs:86-88 */
+    const uint32_t *layers = kind == 0 ? face_layers : kind == 1 ? palm_layers : full_layers;
+    const size_t nl = kind == 2 ? 1 : 2;
+    size_t na = zo_anchors(layers, nl, NULL);
     if (na != nanchors) return 0;
     float *anchors = (float *)malloc(sizeof(float) * 2 * na);
-    zo_anchors(kind == 0 ? face_layers : palm_layers, 2, anchors);
+    zo_anchors(layers, nl, anchors);
     zo_det *tmp = (zo_det *)malloc(sizeof(zo_det) * na);
     size_t n = zo_extract(kind, boxes, confs, na, anchors, in_w, in_h, thresh, tmp, na);
     zo_det *nms = (zo_det *)malloc(sizeof(zo_det) * (n ? n : 1));
@@ -441,9 +446,9 @@ int zo_tracker_update(float *pos, size_t n, const zo_rrect *view_rect, float roi
     return 1;
 }
 
-/* Estimate::angle_radians of the two landmark networks, on view-local positions (n x 3):
- * FaceMesh V1 rotation_radians (mediapipe.rs:146-160): (right_eye 263 - left_eye 33)
- *   .signed_angle_to(X);
+/* Estimate::angle_radians of the landmark networks, on view-local positions (n x 3):
+ * FaceMesh V1 / V2 rotation_radians (mediapipe.rs:146-160, 407-421): (right_eye 263 -
+ *   left_eye 33).signed_angle_to(X);
  * hand landmark rotation_radians (hand/landmark.rs:68-78): (wrist 0 - middle MCP 9)
  *   .signed_angle_to(Y). */
 float zo_landmark_angle(int kind, const float *pos) {

@@ -155,14 +155,27 @@ static int pb_attr_ints(const pb_attr *a, int64_t *out, int cap) {
 #undef REAL
 #undef NN
 
-/* TensorProto: 1 dims, 2 data_type, 4 float_data, 7 int64_data, 8 name, 9 raw_data */
+/* TensorProto: 1 dims, 2 data_type, 4 float_data, 5 int32_data, 7 int64_data, 8 name,
+ * 9 raw_data */
 typedef struct {
     char *name;
     int ndim;
     int64_t dims[6];
     int dtype;
-    pb_slice raw, floats, ints;
+    pb_slice raw, floats, ints, i32s;
 } raw_tensor;
+
+/* IEEE 754 binary16 -> binary64, exact (every half is representable in float and double).
+ * FaceMesh V2 (face_landmarks_detector.onnx) stores its weights as FLOAT16 initializers;
+ * ONNX Runtime upcasts them exactly before the f32 convolutions. */
+static double half_to_double(uint16_t h) {
+    int e = (h >> 10) & 0x1f, m = h & 0x3ff;
+    double v;
+    if (e == 0) v = ldexp((double)m, -24);
+    else if (e == 31) v = m ? NAN : INFINITY;
+    else v = ldexp((double)(m | 0x400), e - 25);
+    return (h & 0x8000) ? -v : v;
+}
 
 static void parse_tensor(pb_slice b, raw_tensor *t) {
     memset(t, 0, sizeof(*t));
@@ -177,6 +190,7 @@ static void parse_tensor(pb_slice b, raw_tensor *t) {
             }
         } else if (f.field == 2) t->dtype = (int)f.v;
         else if (f.field == 4) t->floats = f.bytes;
+        else if (f.field == 5) t->i32s = f.bytes;
         else if (f.field == 7) t->ints = f.bytes;
         else if (f.field == 8) t->name = pb_str(f.bytes);
         else if (f.field == 9) t->raw = f.bytes;
@@ -244,9 +258,29 @@ struct zo_net {
                         while (p < end && k < t->n && pb_varint(&p, end, &v))                   \
                             t->i64[k++] = (int64_t)v;                                           \
                     }                                                                           \
-                } else if (rt.dtype == 10) {                                                    \
-                    snprintf(g_err, sizeof(g_err), "fp16 initializers not supported");          \
-                    return NULL;                                                                \
+                } else if (rt.dtype == 10) { /* FLOAT16: raw bytes or one varint per value */  \
+                    t->f = (REALT *)calloc(t->n ? t->n : 1, sizeof(REALT));                     \
+                    if (rt.raw.p) {                                                             \
+                        if (rt.raw.n != 2 * t->n) {                                             \
+                            snprintf(g_err, sizeof(g_err), "fp16 raw_data size mismatch");      \
+                            return NULL;                                                        \
+                        }                                                                       \
+                        for (size_t i = 0; i < t->n; i++) {                                     \
+                            uint16_t h;                                                         \
+                            memcpy(&h, rt.raw.p + 2 * i, 2);                                    \
+                            t->f[i] = (REALT)half_to_double(h);                                 \
+                        }                                                                       \
+                    } else {                                                                    \
+                        const uint8_t *p = rt.i32s.p, *end = p + rt.i32s.n;                     \
+                        uint64_t v;                                                             \
+                        size_t k = 0;                                                           \
+                        while (p < end && k < t->n && pb_varint(&p, end, &v))                   \
+                            t->f[k++] = (REALT)half_to_double((uint16_t)v);                     \
+                        if (k != t->n) {                                                        \
+                            snprintf(g_err, sizeof(g_err), "fp16 int32_data size mismatch");    \
+                            return NULL;                                                        \
+                        }                                                                       \
+                    }                                                                           \
                 }                                                                               \
                 free(rt.name);                                                                  \
             } else if (f.field == 11 && !n->input_name) {                                       \
@@ -355,4 +389,17 @@ int zo_net_run_f64out(zo_net *n, const float *input, double *const *outputs) {
         if (outputs[o]) memcpy(outputs[o], t->f, sizeof(double) * t->n);
     }
     return 0;
+}
+
+/* Debug/bisection helper: any tensor of the last run of an f64 net by name (copies at most
+ * `cap` values; returns the element count, 0 when absent) and its shape. */
+size_t zo_net_tensor(const zo_net *n, const char *name, double *out, size_t cap, int64_t *shape,
+                     size_t *rank) {
+    if (!n->f64) return 0;
+    tensor_f64 *t = find_f64(n->d, name);
+    if (!t || !t->f) return 0;
+    if (out) memcpy(out, t->f, sizeof(double) * (t->n < cap ? t->n : cap));
+    if (shape) memcpy(shape, t->dims, sizeof(int64_t) * t->ndim);
+    if (rank) *rank = (size_t)t->ndim;
+    return t->n;
 }

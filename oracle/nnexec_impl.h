@@ -26,7 +26,8 @@ typedef struct {
 } NN(node);
 
 struct NN(net_s) {
-    NN(tensor) *vals; /* initializers + computed values */
+    NN(tensor) **vals; /* initializers + computed values; each individually allocated, so a
+                        * tensor pointer stays valid while later values are pushed */
     size_t nvals, cap;
     NN(node) *nodes;
     size_t nnodes;
@@ -39,17 +40,17 @@ struct NN(net_s) {
 
 static NN(tensor) *NN(find)(struct NN(net_s) *n, const char *name) {
     for (size_t i = n->nvals; i-- > 0;)
-        if (strcmp(n->vals[i].name, name) == 0) return &n->vals[i];
+        if (strcmp(n->vals[i]->name, name) == 0) return n->vals[i];
     return NULL;
 }
 
 static NN(tensor) *NN(push)(struct NN(net_s) *n, const char *name) {
     if (n->nvals == n->cap) {
         n->cap = n->cap ? n->cap * 2 : 256;
-        n->vals = (NN(tensor) *)realloc(n->vals, n->cap * sizeof(NN(tensor)));
+        n->vals = (NN(tensor) **)realloc(n->vals, n->cap * sizeof(NN(tensor) *));
     }
-    NN(tensor) *t = &n->vals[n->nvals++];
-    memset(t, 0, sizeof(*t));
+    NN(tensor) *t = (NN(tensor) *)calloc(1, sizeof(NN(tensor)));
+    n->vals[n->nvals++] = t;
     t->name = strdup(name);
     return t;
 }
@@ -466,10 +467,11 @@ static int NN(exec_node)(struct NN(net_s) *n, const NN(node) *nd) {
 
 static void NN(clear_dynamic)(struct NN(net_s) *n) {
     while (n->nvals > n->nstatic) {
-        NN(tensor) *t = &n->vals[--n->nvals];
+        NN(tensor) *t = n->vals[--n->nvals];
         free(t->name);
         free(t->f);
         free(t->i64);
+        free(t);
     }
 }
 

@@ -97,6 +97,8 @@ size_t zo_net_output_shape(const zo_net *n, size_t idx, int64_t *shape);
 /* input: NCHW 1x3xHxW float; outputs: float arrays sized per output shape. 0 on success */
 int zo_net_run(zo_net *n, const float *input, float *const *outputs);
 const char *zo_net_error(void);
+size_t zo_net_tensor(const zo_net *n, const char *name, double *out, size_t cap, int64_t *shape,
+                     size_t *rank);
 
 #ifdef __cplusplus
 }

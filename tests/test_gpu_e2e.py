@@ -54,7 +54,13 @@ CASES = {
              O.FACEMESH, 0.3, 8),
     "hand": ("palm_detection_lite", "hand_landmark_lite", 192, 224, 0.0, O.PALM,
              O.HAND, 0.4, 5),
+    # BlazeFace full range (192^2, 2304 anchors) -> FaceMesh V2 (256^2, 478
+    # points, fp16 weights) through the same face pipeline
+    "face_next": ("face_detection_full_range", "face_landmarks_detector", 192, 256, -1.0,
+                  O.FACE_FULL, O.FACEMESH_V2, 0.3, 8),
 }
+PIPELINE_ARGS = {"face": ("face", {}), "hand": ("hand", {}),
+                 "face_next": ("face", {"detector": "face_full", "landmarker": "facemesh_v2"})}
 
 
 def face_patch():
@@ -106,22 +112,23 @@ def rrect_close(got, want, per_px):
     return d_ang, d_px
 
 
-@pytest.mark.parametrize("kind", ["face", "hand"])
+@pytest.mark.parametrize("kind", ["face", "hand", "face_next"])
 def test_pipeline_vs_oracle_1080p(H_, kind):
     from zaru_amd._lib import DeviceBuffer
 
     det_m, lm_m, din, lin, lo, okind, lkind, pad, n_check = CASES[kind]
-    frames, forced = frames_for(kind, BATCH, 101 if kind == "face" else 102)
+    base, nets = PIPELINE_ARGS[kind]
+    frames, forced = frames_for(base, BATCH, 102 if kind == "hand" else 101)
     buf = DeviceBuffer.from_array(frames)
     fb = H * W * 4
     flist = [(buf.ptr + i * fb, W, H, W * 4) for i in range(BATCH)]
-    per_frame = 1 if kind == "face" else 4
+    per_frame = 1 if base == "face" else 4
     runs = {}
     for loss in (0.5, 0.0):
-        p = H_.DetectTrackPipeline(kind, 0, 8, per_frame, 3, True, loss)
+        p = H_.DetectTrackPipeline(base, 0, 8, per_frame, 3, True, loss, **nets)
         p.run(flist, forced)
         runs[loss] = p
-        if kind == "face":
+        if base == "face":
             break  # every face ROI tracks at 0.5 already
     p = runs[0.5]
 
@@ -175,7 +182,7 @@ def test_pipeline_vs_oracle_1080p(H_, kind):
         want, upd, nxt = O.tracker_update(pos, vr, rad, est_angle, pad)
         per_px = lrect.w / lin  # frame px per network-input px
         # the estimate angle is well-conditioned only when its two landmarks are apart
-        a, b = (263, 33) if lkind == O.FACEMESH else (0, 9)
+        a, b = (0, 9) if lkind == O.HAND else (263, 33)
         sep = float(np.hypot(*(pos[a, :2] - pos[b, :2]))) / per_px
         stats["rois"] += 1
         for loss, q in runs.items():

@@ -19,7 +19,11 @@ MODELS = {
     "face_landmark": (192, -1.0, 1.0),
     "palm_detection_lite": (192, 0.0, 1.0),
     "hand_landmark_lite": (224, 0.0, 1.0),
+    # SURVEY 8(f)-1 (fixtures in next_models.npz)
+    "face_detection_full_range": (192, -1.0, 1.0),
+    "face_landmarks_detector": (256, -1.0, 1.0),
 }
+NEXT = ("face_detection_full_range", "face_landmarks_detector")
 ABS_TOL = 2e-3
 
 
@@ -36,7 +40,7 @@ def codes_to_input(codes, lo, hi):
 
 @pytest.mark.parametrize("model", list(MODELS))
 def test_model_vs_f64_golden(nets, golden_dir, model):
-    g = np.load(os.path.join(golden_dir, "models_f64.npz"))
+    g = np.load(os.path.join(golden_dir, "next_models.npz" if model in NEXT else "models_f64.npz"))
     s, lo, hi = MODELS[model]
     x = np.stack([codes_to_input(g[f"{model}/{k}/codes"], lo, hi) for k in range(2)])
     outs = nets[model].estimate(x)
@@ -45,7 +49,7 @@ def test_model_vs_f64_golden(nets, golden_dir, model):
         err = float(np.abs(o - want).max())
         print(f"{model} out{oi}: max|gpu - f64| = {err:.3e}")
         assert err <= ABS_TOL, (model, oi, err)
-    if model in ("face_landmark", "hand_landmark_lite"):
+    if model in ("face_landmark", "hand_landmark_lite", "face_landmarks_detector"):
         lm = outs[0].reshape(2, -1, 3)
         want = np.stack([g[f"{model}/{k}/out0"].reshape(-1, 3) for k in range(2)])
         l2 = np.sqrt(((lm[..., :2] - want[..., :2]) ** 2).sum(-1)).max()
@@ -107,6 +111,40 @@ def test_facemesh_rotations(nets, golden_dir, kat):
         assert abs(ang - case["expect_deg"]) < m["angle_tol_deg"]
         l2 = np.sqrt(((lm[:, :2] - g["landmarks"][i][:, :2]) ** 2).sum(-1)).max()
         assert l2 <= 1e-3, l2
+
+
+def test_detects_face_full_range(nets, golden_dir, kat):
+    """face/detection.rs:164-173's bar applied to FullRangeNetwork (face/detection.rs:61-94) on
+    the same image, letterboxed to 192^2, through the HIP runner."""
+    g = np.load(os.path.join(golden_dir, "next_models.npz"))
+    x = codes_to_input(g["full_linus/codes"], -1.0, 1.0)[None]
+    reg, cls = nets["face_detection_full_range"].estimate(x)
+    assert np.abs(reg - g["full_linus/regressors"]).max() <= ABS_TOL
+    assert np.abs(cls - g["full_linus/classificators"]).max() <= ABS_TOL
+    w, h = (int(v) for v in g["full_linus/image_wh"])
+    dets = O.detect_post(O.FACE_FULL, reg[0], cls[0], w, h, 192, 192)
+    m = kat["models"]["detects_face"]
+    assert dets and dets[0].conf >= m["min_conf"]
+    assert abs(math.degrees(dets[0].angle)) < m["max_abs_angle_deg"]
+
+
+def test_facemesh_v2_rotations(nets, golden_dir, kat):
+    """mediapipe.rs:603-624's bars (confidence, eye-line angle) applied to FaceMeshV2
+    (mediapipe.rs:81-116, 478 points, fp16 weights upcast at load), plus tongue_out and the
+    landmark L2 against the f64 oracle."""
+    g = np.load(os.path.join(golden_dir, "next_models.npz"))
+    x = codes_to_input(g["v2_linus/codes"], -1.0, 1.0)
+    lms, flags, tongue = nets["face_landmarks_detector"].estimate(x)
+    m = kat["models"]["facemesh"]
+    for i, case in enumerate(m["cases"]):
+        lm = lms[i].reshape(478, 3)
+        assert O.sigmoid(float(flags[i].reshape(-1)[0])) > m["min_conf"]
+        d = lm[263, :2] - lm[33, :2]
+        ang = math.degrees(O.signed_angle_to((float(d[0]), float(d[1])), (1.0, 0.0)))
+        assert abs(ang - case["expect_deg"]) < m["angle_tol_deg"]
+        l2 = np.sqrt(((lm[:, :2] - g["v2_linus/landmarks"][i][:, :2]) ** 2).sum(-1)).max()
+        assert l2 <= 1e-3, l2
+        assert abs(float(tongue[i].reshape(-1)[0]) - float(g["v2_linus/tongue_out"][i])) <= 1e-5
 
 
 def _random_views(rng, n, w, h):

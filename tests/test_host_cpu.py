@@ -121,3 +121,32 @@ def test_candidate_floor_is_conservative():
         xs = np.nextafter(np.float32(lf), np.float32(-np.inf)) - np.arange(0, 2000, dtype=np.float32) * np.float32(1e-5)
         assert all(O.sigmoid(float(x)) < np.float32(t) for x in xs[:200])
         assert O.sigmoid(lf) < np.float32(t)
+
+
+def test_full_range_anchors_and_decode_match_oracle():
+    """FullRangeNetwork::extract (face/detection.rs:80-94: 48x48 anchors, 16 params, 192^2
+    input) + NMS + map through the C++ host vs the oracle, bit-exact on seeded raw tensors
+    with planted clusters."""
+    import oracle as O
+    assert np.array_equal(H.anchors("face_full"), O.anchors(O.FACE_FULL_LAYERS))
+    assert H.anchors("face_full").shape == (2304, 2)
+    rng = np.random.default_rng(0x5A525510)
+    for case in range(6):
+        boxes = rng.normal(0, 3, size=(2304, 16)).astype(np.float32)
+        confs = rng.normal(-6, 1, size=(2304,)).astype(np.float32)
+        for _ in range(3 + case):
+            a = int(rng.integers(0, 2304))
+            for j in [a, *rng.integers(max(0, a - 12), min(2304, a + 12), size=5).tolist()]:
+                confs[j] = np.float32(rng.uniform(0.1, 4.0))
+                boxes[j, 0:2] = rng.normal(0, 1.5, 2)
+                boxes[j, 2:4] = float(rng.uniform(8, 60)) * rng.uniform(0.85, 1.15, 2)
+        iw, ih = int(rng.integers(64, 2000)), int(rng.integers(64, 2000))
+        got = H.detect_post("face_full", boxes, confs, iw, ih)
+        want = O.detect_post(O.FACE_FULL, boxes, confs, iw, ih, 192, 192)
+        assert len(got) == len(want) > 0
+        for d, w in zip(got, want):
+            assert np.float32(d.confidence()) == np.float32(w.conf)
+            assert np.float32(d.angle()) == np.float32(w.angle)
+            assert d.bounding_rect().tuple() == tuple(float(np.float32(v)) for v in w.rect.tuple())
+            for k, (x, y) in enumerate(d.keypoints()):
+                assert (np.float32(x), np.float32(y)) == (np.float32(w.kp[k][0]), np.float32(w.kp[k][1]))

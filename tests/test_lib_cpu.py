@@ -59,6 +59,21 @@ def test_plan_compiles_and_fuses(models_dir, model, launches, chained):
     assert len(fused) == launches - chained + (1 if chained else 0)
 
 
+@pytest.mark.parametrize("model,outputs", [
+    ("face_detection_full_range", ["reshaped_regressor_face_4", "reshaped_classifier_face_4"]),
+    ("face_landmarks_detector", None)])
+def test_next_models_compile(models_dir, model, outputs):
+    """BlazeFace full range (Resize linear FPN) and FaceMesh V2 (fp16 weights)
+    lower to the same fused kernels, with no standalone element-wise pass."""
+    txt = _lib.plan_describe(open(os.path.join(models_dir, model + ".onnx"), "rb").read())
+    steps = [l for l in txt.splitlines() if l.split(" ")[0] in KINDS]
+    assert steps and not [l for l in steps if l.startswith("elt")]
+    for o in outputs or []:
+        assert f"output {o}" in txt
+    if model == "face_landmarks_detector":
+        assert txt.count("\noutput ") == 3 or txt.count("output ") >= 3
+
+
 def test_plan_output_selection(models_dir):
     data = open(os.path.join(models_dir, "face_landmark.onnx"), "rb").read()
     full = _lib.plan_describe(data)
@@ -171,3 +186,26 @@ def test_malformed_tensor_is_a_model_error(case):
     with pytest.raises(_lib.ZaruError) as e:
         _lib.plan_describe(m)
     assert e.value.code == -2, str(e.value)
+
+
+@pytest.mark.parametrize("model", ["face_detection_short_range", "face_landmark", "palm_detection_lite",
+                                   "hand_landmark_lite", "face_detection_full_range",
+                                   "face_landmarks_detector"])
+def test_plan_reads_only_produced_tensors(models_dir, model):
+    """Every launch reads tensors (its input and its fused shortcut) that an earlier launch wrote.
+    BlazeFace full range fuses an FPN Add into a conv that precedes, in ONNX order, the Resize
+    producing its shortcut; the compiler must run that conv after the Resize."""
+    import re
+    txt = _lib.plan_describe(open(os.path.join(models_dir, model + ".onnx"), "rb").read())
+    produced = set()
+    for line in txt.splitlines():
+        if line.split(" ")[0] not in KINDS:
+            continue
+        reads = [re.search(r" in=(\S+)", line).group(1)]
+        m = re.search(r" in2=(\S+)", line)
+        if m and m.group(1) != "-":
+            reads.append(m.group(1))
+        for r in reads:
+            t = r.split("[")[0]
+            assert t == "in0" or t in produced, (model, line)
+        produced.add(re.search(r" out=(\S+)", line).group(1).split("[")[0])

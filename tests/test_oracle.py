@@ -4,6 +4,7 @@ Every case here comes from a #[test] in /root/reference (see tools/make_golden.p
 file:line of each).  The oracle is the checker for the HIP path, so it is pinned first.
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -141,3 +142,85 @@ def test_decode_cases_self_consistent(golden_dir):
         assert len(dets) == len(want)
         for d, w in zip(dets, want):
             assert d.conf == w[0] and d.angle == w[1] and d.rect.tuple() == tuple(w[2:6])
+
+
+# ---------------------------------------------------------------- SURVEY 8(f)-1 networks
+def test_full_range_detects_face(kat, golden_dir, models_dir):
+    """face/detection.rs:164-173's bar applied to FullRangeNetwork (face/detection.rs:61-94:
+    one 48x48 anchor layer, 192^2 input) on the same sad_linus.jpg letterbox."""
+    g = np.load(f"{golden_dir}/next_models.npz")
+    x = g["full_linus/codes"].astype(np.float32) * np.float32(np.float32(2.0) / np.float32(255.0)) - 1.0
+    net = O.Net(f"{models_dir}/face_detection_full_range.onnx", f64=True)
+    reg, cls = net.run(x[None].astype(np.float32))
+    assert reg.shape == (1, 2304, 16) and cls.shape == (1, 2304, 1)
+    w, h = (int(v) for v in g["full_linus/image_wh"])
+    dets = O.detect_post(O.FACE_FULL, reg[0], cls[0], w, h, 192, 192)
+    m = kat["models"]["detects_face"]
+    assert dets and dets[0].conf >= m["min_conf"]
+    assert abs(math.degrees(dets[0].angle)) < m["max_abs_angle_deg"]
+    assert np.allclose(reg, g["full_linus/regressors"], atol=2e-4)
+
+
+def test_facemesh_v2_rotations(kat, golden_dir, models_dir):
+    """mediapipe.rs:603-624's bars applied to FaceMeshV2 (mediapipe.rs:81-116): the fp16
+    initializers (upcast exactly) give a confident mesh whose eye line follows the view."""
+    g = np.load(f"{golden_dir}/next_models.npz")
+    net = O.Net(f"{models_dir}/face_landmarks_detector.onnx", f64=False)
+    m = kat["models"]["facemesh"]
+    adj = np.float32(np.float32(2.0) / np.float32(255.0))
+    for i, case in enumerate(m["cases"]):
+        x = g["v2_linus/codes"][i].astype(np.float32) * adj - np.float32(1.0)
+        lm, flag, tongue = net.run(x[None])
+        lm = lm.reshape(478, 3)
+        assert O.landmark_confidence(O.FACEMESH_V2, (lm, flag)) > m["min_conf"]
+        ang = math.degrees(O.landmark_angle(O.FACEMESH_V2, lm))
+        assert abs(ang - case["expect_deg"]) < m["angle_tol_deg"]
+        assert np.abs(lm - g["v2_linus/landmarks"][i]).max() < 1e-3
+        assert 0.0 <= float(tongue.reshape(-1)[0]) <= 1.0  # sigmoid inside the graph
+
+
+def test_fp16_initializers_upcast_exactly(models_dir):
+    """The f32 and f64 interpreters read the same fp16 weights: their outputs differ only by
+    f32 evaluation noise, far below any fp16 rounding step of the weights (2^-11 relative)."""
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "next_models.npz"))
+    x = g["face_landmarks_detector/0/codes"].astype(np.float32) * np.float32(2.0 / 255.0) - 1.0
+    lo = O.Net(f"{models_dir}/face_landmarks_detector.onnx", f64=False).run(x[None].astype(np.float32))
+    for oi, o in enumerate(lo):
+        want = g[f"face_landmarks_detector/0/out{oi}"]
+        assert np.abs(o - want).max() <= 2e-4 * max(1.0, float(np.abs(want).max())), oi
+
+
+ASAN_CHILD = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+import oracle as O
+O.LIB_PATH = sys.argv[2]
+sizes = {"face_detection_short_range": 128, "face_landmark": 192, "palm_detection_lite": 192,
+         "hand_landmark_lite": 224, "face_detection_full_range": 192, "face_landmarks_detector": 256}
+for m, s in sizes.items():
+    n = O.Net(f"{sys.argv[1]}/zaru_amd/models/{m}.onnx", f64=False)
+    for k in range(2):
+        n.run(np.random.default_rng(k).uniform(-1, 1, (1, 3, s, s)).astype(np.float32))
+print("clean")
+"""
+
+
+def test_oracle_interpreter_is_memory_clean(tmp_path):
+    """The checker itself under AddressSanitizer (host code only): every model, two runs each.
+    (A value-table realloc once left tensor pointers dangling mid-operator.)"""
+    import shutil
+    import subprocess
+    import sys
+    asan = subprocess.run(["gcc", "-print-file-name=libasan.so"], capture_output=True, text=True).stdout.strip()
+    if not shutil.which("gcc") or not os.path.isabs(asan):
+        pytest.skip("no gcc/libasan")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = str(tmp_path / "liboracle_asan.so")
+    subprocess.run(["gcc", "-shared", "-fPIC", "-O1", "-g", "-fsanitize=address", "-fno-omit-frame-pointer",
+                    "-ffp-contract=off", "-o", lib, f"{repo}/oracle/geom.c", f"{repo}/oracle/nnexec.c", "-lm"],
+                   check=True)
+    env = dict(os.environ, LD_PRELOAD=asan, ASAN_OPTIONS="detect_leaks=0")
+    r = subprocess.run([sys.executable, "-c", ASAN_CHILD, repo, lib], env=env, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0 and "clean" in r.stdout, r.stderr[-3000:]

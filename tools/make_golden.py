@@ -283,7 +283,80 @@ def decode_cases():
     np.savez_compressed(os.path.join(GOLD, "decode_cases.npz"), **cases)
 
 
+# ------------------------------------------------------------------ SURVEY 8(f)-1 networks
+NEXT_SPECS = {  # BlazeFace full range (face/detection.rs:61-94), FaceMesh V2 (mediapipe.rs:81-116)
+    "face_detection_full_range": ("face_detection_full_range.onnx", 192, -1.0, 1.0),
+    "face_landmarks_detector": ("face_landmarks_detector.onnx", 256, -1.0, 1.0),
+}
+
+
+def next_models():
+    """next_models.npz: F2 (two seeded inputs -> f64 outputs) for both networks, plus the
+    reference's qualitative model checks re-run on its own images: the full-range detector
+    on the sad_linus.jpg letterbox (192^2) and FaceMesh V2 on sad_linus_cropped.jpg at
+    0 / +-10 degrees (256^2).  The reference tests only ShortRangeNetwork / FaceMeshV1 with
+    these images (face/detection.rs:164-173, mediapipe.rs:575-624); the same bars are applied
+    here to the two networks that share their Network trait and extract code."""
+    out = {}
+    for mi, (name, (fn, s, lo, hi)) in enumerate(NEXT_SPECS.items()):
+        net = O.Net(os.path.join(MODELS, fn), f64=True)
+        rng = np.random.default_rng(0x5A525504 + mi)
+        for k in range(2):
+            codes = rng.integers(0, 256, size=(3, s, s), dtype=np.uint8)
+            adj = np.float32((np.float32(hi) - np.float32(lo)) / np.float32(255.0))
+            x = codes.astype(np.float32) * adj + np.float32(lo)
+            outs = net.run(x[None], as_f64=True)
+            out[f"{name}/{k}/codes"] = codes
+            for oi, o in enumerate(outs):
+                out[f"{name}/{k}/out{oi}"] = o.astype(np.float32)
+        print("next_models:", name, [o.shape for o in outs])
+    # full range on the sad_linus letterbox
+    img = load_rgba("sad_linus.jpg")
+    h, w = img.shape[:2]
+    rect = O.grow_to_fit_aspect(O.Rect.from_top_left(0, 0, w, h), 192, 192)
+    view = O.view_compose(O.view_full(w, h), rect)
+    x = O.preproc(img, view, 192, 192, -1.0, 1.0)
+    net = O.Net(os.path.join(MODELS, "face_detection_full_range.onnx"), f64=True)
+    reg, cls = net.run(x[None], as_f64=True)
+    dets = O.detect_post(O.FACE_FULL, reg[0].astype(np.float32), cls[0].astype(np.float32),
+                         w, h, 192, 192)
+    print("sad_linus full range:", [(d.conf, math.degrees(d.angle)) for d in dets])
+    out["full_linus/codes"] = to_codes(x, -1.0, 1.0)
+    out["full_linus/image_wh"] = np.array([w, h])
+    out["full_linus/regressors"] = reg.astype(np.float32)
+    out["full_linus/classificators"] = cls.astype(np.float32)
+    # FaceMesh V2 on the cropped image, rotated views as in mediapipe.rs:603-624
+    img = load_rgba("sad_linus_cropped.jpg")
+    h, w = img.shape[:2]
+    net = O.Net(os.path.join(MODELS, "face_landmarks_detector.onnx"), f64=True)
+    codes, lms, flags, tongue, degs = [], [], [], [], []
+    for deg in (0.0, 10.0, -10.0):
+        rad = deg_to_rad_f32(abs(deg)) * (1 if deg >= 0 else -1)
+        v1 = O.view_compose(O.view_full(w, h), O.RRect(O.Rect.from_top_left(0, 0, w, h), rad))
+        lrect = O.grow_to_fit_aspect(O.Rect.from_top_left(0, 0, v1.rect.w, v1.rect.h), 256, 256)
+        v2 = O.view_compose(v1, lrect)
+        x = O.preproc(img, v2, 256, 256, -1.0, 1.0)
+        lm, flag, tg = net.run(x[None], as_f64=True)
+        codes.append(to_codes(x, -1.0, 1.0))
+        lms.append(lm.reshape(478, 3).astype(np.float32))
+        flags.append(np.float32(flag.reshape(-1)[0]))
+        tongue.append(np.float32(tg.reshape(-1)[0]))
+        degs.append(deg)
+        d = lms[-1][263, :2] - lms[-1][33, :2]
+        print("sad_linus V2", deg, "flag", O.sigmoid(flags[-1]),
+              "angle", math.degrees(O.signed_angle_to((float(d[0]), float(d[1])), (1.0, 0.0))))
+    out["v2_linus/codes"] = np.stack(codes)
+    out["v2_linus/landmarks"] = np.stack(lms)
+    out["v2_linus/flag_logit"] = np.array(flags, np.float32)
+    out["v2_linus/tongue_out"] = np.array(tongue, np.float32)
+    out["v2_linus/view_deg"] = np.array(degs, np.float32)
+    np.savez_compressed(os.path.join(GOLD, "next_models.npz"), **out)
+
+
 def main():
+    if sys.argv[1:] == ["next"]:
+        next_models()
+        return
     os.makedirs(GOLD, exist_ok=True)
     with open(os.path.join(GOLD, "reference_kat.json"), "w") as f:
         json.dump(reference_kat(), f, indent=1)
@@ -292,6 +365,7 @@ def main():
     sad_linus_mesh()
     models_f64()
     decode_cases()
+    next_models()
 
 
 if __name__ == "__main__":

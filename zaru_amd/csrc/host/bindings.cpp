@@ -37,19 +37,22 @@ py::dict estimate_dict(const Estimate &e) {
     d["landmarks"] = p;
     d["confidence"] = e.confidence;
     d["raw_handedness"] = e.raw_handedness;
+    d["tongue_out"] = e.tongue_out;
     return d;
 }
 
 DetectorNetwork detector_net(const std::string &name) {
     if (name == "face") return DetectorNetwork::short_range_face();
+    if (name == "face_full") return DetectorNetwork::full_range_face();
     if (name == "palm") return DetectorNetwork::palm_lite();
-    throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "detector network must be 'face' or 'palm'");
+    throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "detector network must be 'face', 'face_full' or 'palm'");
 }
 
 LandmarkNetwork landmark_net(const std::string &name) {
     if (name == "facemesh") return LandmarkNetwork::face_mesh_v1();
+    if (name == "facemesh_v2") return LandmarkNetwork::face_mesh_v2();
     if (name == "hand") return LandmarkNetwork::hand_lite();
-    throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "landmark network must be 'facemesh' or 'hand'");
+    throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "landmark network must be 'facemesh', 'facemesh_v2' or 'hand'");
 }
 
 // Detector::detect_impl after inference on raw outputs (detection.rs:231-267)
@@ -57,6 +60,7 @@ std::vector<Detection> detect_post(const std::string &net, py::array_t<float, py
                                    py::array_t<float, py::array::c_style> logits, uint32_t img_w,
                                    uint32_t img_h, float thresh, float iou) {
     DetectorNetwork dn = detector_net(net);
+    // network input sizes: short range 128, full range / palm 192 (the ONNX input shapes)
     const uint32_t s = dn.kind == NetworkKind::FaceDetectionShortRange ? 128 : 192;
     if ((size_t)logits.size() != dn.anchors().size() || (size_t)boxes.size() != dn.anchors().size() * dn.params)
         throw ZaruError(ZR_ERR_SHAPE, "raw outputs do not match the network's anchors");
@@ -276,10 +280,15 @@ PYBIND11_MODULE(_zaru_host, m) {
 
     py::class_<DetectTrackPipeline>(m, "DetectTrackPipeline")
         .def(py::init([](const std::string &kind, int device, int threads, uint32_t max_rois,
-                         uint32_t sub_batches, bool stream_per_sub_batch, float loss_threshold) {
+                         uint32_t sub_batches, bool stream_per_sub_batch, float loss_threshold,
+                         const std::string &detector, const std::string &landmarker) {
                  PipelineConfig c = kind == "hand" ? PipelineConfig::hand() : PipelineConfig::face();
                  if (kind != "hand" && kind != "face")
                      throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "pipeline kind must be 'face' or 'hand'");
+                 // network overrides within a kind: BlazeFace full range / FaceMesh V2
+                 //  run through the same pipeline as config 3
+                 if (!detector.empty()) c.detector = detector_net(detector);
+                 if (!landmarker.empty()) c.landmarker = landmark_net(landmarker);
                  c.max_rois_per_frame = max_rois;
                  c.sub_batches = sub_batches;
                  c.stream_per_sub_batch = stream_per_sub_batch;
@@ -288,7 +297,8 @@ PYBIND11_MODULE(_zaru_host, m) {
              }), py::arg("kind") = "face", py::arg("device") = 0, py::arg("threads") = 8,
              py::arg("max_rois_per_frame") = 8, py::arg("sub_batches") = 2,
              py::arg("stream_per_sub_batch") = true,
-             py::arg("loss_threshold") = LandmarkTracker::DEFAULT_LOSS_THRESHOLD)
+             py::arg("loss_threshold") = LandmarkTracker::DEFAULT_LOSS_THRESHOLD,
+             py::arg("detector") = "", py::arg("landmarker") = "")
         // frames: list of (device ptr, width, height, row_stride); forced: per frame list of
         // (cx, cy, w, h, rad) ROIs used when the frame has no detection
         .def("run", [](DetectTrackPipeline &p, const std::vector<std::tuple<uint64_t, uint32_t, uint32_t, uint64_t>> &frames,

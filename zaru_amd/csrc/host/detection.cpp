@@ -97,6 +97,15 @@ DetectorNetwork DetectorNetwork::short_range_face() {
     return n;
 }
 
+DetectorNetwork DetectorNetwork::full_range_face() {
+    DetectorNetwork n;
+    n.kind = NetworkKind::FaceDetectionFullRange;
+    n.layers = {{1, 48, 48}};  // 2304 anchors (face/detection.rs:86-88)
+    n.params = 16;
+    n.keypoints = 6;
+    return n;
+}
+
 DetectorNetwork DetectorNetwork::palm_lite() {
     DetectorNetwork n;
     n.kind = NetworkKind::PalmDetectionLite;
@@ -123,7 +132,7 @@ Detection DetectorNetwork::decode(uint32_t anchor, const float *b, float confide
     d.rect = Rect::from_center(center.x, center.y, b[2], b[3]);
     for (int k = 0; k < keypoints; k++)  // quirk kept: offset by centre * input size
         d.keypoints.push_back(Vec2{b[4 + 2 * k], b[5 + 2 * k]} + center * input_size);
-    if (kind == NetworkKind::FaceDetectionShortRange) {
+    if (is_face_detector(kind)) {
         // left eye -> right eye against +X (face/detection.rs:151-154)
         d.angle = signed_angle_to(d.keypoints[1] - d.keypoints[0], Vec2{1.f, 0.f});
     } else {

@@ -50,6 +50,7 @@ struct DetectorNetwork {
     int params;    // 16 face / 18 palm
     int keypoints;  // 6 / 7
     static DetectorNetwork short_range_face();  // face/detection.rs:30-59
+    static DetectorNetwork full_range_face();   // face/detection.rs:61-94
     static DetectorNetwork palm_lite();         // hand/detection.rs:49-75
     const std::vector<Vec2> &anchors() const;
     // extract_detection (face/detection.rs:124-157, hand/detection.rs:144-179)

@@ -4,6 +4,7 @@
 namespace zh {
 
 LandmarkNetwork LandmarkNetwork::face_mesh_v1() { return {NetworkKind::FaceMeshV1, 468}; }
+LandmarkNetwork LandmarkNetwork::face_mesh_v2() { return {NetworkKind::FaceMeshV2, 478}; }
 LandmarkNetwork LandmarkNetwork::hand_lite() { return {NetworkKind::HandLandmarkLite, 21}; }
 
 void extract_landmarks(const LandmarkNetwork &net, const float *const *outs, Estimate &e) {
@@ -11,6 +12,9 @@ void extract_landmarks(const LandmarkNetwork &net, const float *const *outs, Est
     e.positions.assign(outs[0], outs[0] + 3 * n);
     if (net.kind == NetworkKind::FaceMeshV1) {
         e.confidence = sigmoid(outs[1][0]);  // face_flag, mediapipe.rs:60
+    } else if (net.kind == NetworkKind::FaceMeshV2) {
+        e.confidence = sigmoid(outs[1][0]);  // face_flag, mediapipe.rs:100
+        e.tongue_out = outs[2][0];           // mediapipe.rs:103
     } else {
         e.confidence = outs[1][0];  // presence (sigmoid inside the graph)
         e.raw_handedness = outs[2][0];
@@ -19,7 +23,7 @@ void extract_landmarks(const LandmarkNetwork &net, const float *const *outs, Est
 }
 
 float estimate_angle(const LandmarkNetwork &net, const Estimate &e) {
-    if (net.kind == NetworkKind::FaceMeshV1) return signed_angle_to(e.xy(263) - e.xy(33), Vec2{1.f, 0.f});
+    if (is_face_mesh(net.kind)) return signed_angle_to(e.xy(263) - e.xy(33), Vec2{1.f, 0.f});
     return signed_angle_to(e.xy(0) - e.xy(9), Vec2{0.f, 1.f});
 }
 

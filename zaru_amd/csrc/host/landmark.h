@@ -13,8 +13,9 @@ namespace zh {
 
 struct LandmarkNetwork {
     NetworkKind kind;
-    int num_landmarks;  // 468 / 21
+    int num_landmarks;  // 468 / 478 / 21
     static LandmarkNetwork face_mesh_v1();
+    static LandmarkNetwork face_mesh_v2();  // mediapipe.rs:81-116
     static LandmarkNetwork hand_lite();
 };
 
@@ -23,6 +24,7 @@ struct Estimate {
     std::vector<float> positions;  // n * 3
     float confidence = 0.f;        // face_flag (sigmoid) / hand presence (Confidence trait)
     float raw_handedness = 0.f;    // hand only
+    float tongue_out = 0.f;        // FaceMesh V2 blendshape (sigmoid inside the graph)
     std::vector<float> world;      // hand metric landmarks (Identity_3), n * 3
     size_t size() const { return positions.size() / 3; }
     Vec2 xy(size_t i) const { return {positions[3 * i], positions[3 * i + 1]}; }

@@ -123,6 +123,14 @@ std::shared_ptr<const Cnn> network_cnn(NetworkKind k, int device) {
         file = "hand_landmark_lite.onnx";
         cm = {0.f, 1.f};
         break;
+    case NetworkKind::FaceDetectionFullRange:  // face/detection.rs:67-79
+        file = "face_detection_full_range.onnx";
+        cm = {-1.f, 1.f};
+        break;
+    case NetworkKind::FaceMeshV2:  // face/landmark/mediapipe.rs:86-97 (fp16 weights, upcast at load)
+        file = "face_landmarks_detector.onnx";
+        cm = {-1.f, 1.f};
+        break;
     }
     auto nn = std::make_shared<NeuralNetwork>(read_file(dir + "/" + file), std::vector<uint32_t>{}, device);
     auto cnn = std::make_shared<const Cnn>(nn, cm);

@@ -1,6 +1,7 @@
 // networks.h -- Cnn / ColorMapper (crates/zaru/src/nn/mod.rs:30-168) and the four hot-path
-// network wrappers: face::detection::ShortRangeNetwork, face::landmark::mediapipe::FaceMeshV1,
-// hand::detection::LiteNetwork, hand::landmark::LiteNetwork.
+// network wrappers: face::detection::{ShortRangeNetwork, FullRangeNetwork},
+// face::landmark::mediapipe::{FaceMeshV1, FaceMeshV2}, hand::detection::LiteNetwork,
+// hand::landmark::LiteNetwork.
 #pragma once
 #include <memory>
 #include <string>
@@ -41,7 +42,19 @@ class Cnn {
 
 zr_view to_zr_view(const ViewData &v);
 
-enum class NetworkKind { FaceDetectionShortRange, FaceMeshV1, PalmDetectionLite, HandLandmarkLite };
+enum class NetworkKind {
+    FaceDetectionShortRange,
+    FaceMeshV1,
+    PalmDetectionLite,
+    HandLandmarkLite,
+    FaceDetectionFullRange,
+    FaceMeshV2,
+};
+
+inline bool is_face_mesh(NetworkKind k) { return k == NetworkKind::FaceMeshV1 || k == NetworkKind::FaceMeshV2; }
+inline bool is_face_detector(NetworkKind k) {
+    return k == NetworkKind::FaceDetectionShortRange || k == NetworkKind::FaceDetectionFullRange;
+}
 
 // Lazily loaded, process-wide CNN per (network, device) -- the reference's
 // `static MODEL: OnceLock<Cnn>` (e.g. face/detection.rs:36-45).

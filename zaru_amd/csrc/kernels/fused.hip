@@ -1066,6 +1066,21 @@ const char *launch_dwpw(const DwPwParams &p, hipStream_t s) {
             best_wgs = wgs;
         }
     }
+    if (!best) {
+        // no tile height wastes <= 1/3 of its rows without an M split (e.g. Mpad = 160, the
+        // 144-channel blocks of BlazeFace full range): the unsplit tile with the fewest padded
+        // rows, else the tallest split one
+        int waste = 1 << 30;
+        for (const DwPwLayout &l : kLayouts) {
+            const int mb = (p.g.Mpad + l.bm() - 1) / l.bm();
+            if (mb > 1 && l.bm() < 256) continue;
+            const int w = mb * l.bm() - p.g.Mpad;
+            if (w < waste) {
+                waste = w;
+                best = &l;
+            }
+        }
+    }
     if (p.k == 3) return p.stride == 1 ? dwpw_layout<3, 1>(p, *best, s) : dwpw_layout<3, 2>(p, *best, s);
     return p.stride == 1 ? dwpw_layout<5, 1>(p, *best, s) : dwpw_layout<5, 2>(p, *best, s);
 }

@@ -627,6 +627,20 @@ bool Compiler::lower_add(const OnnxNode &nd) {
             y.tensor = p.tensor;
         }
         p.tensor = -1;
+        // The shortcut may come from a step emitted after the conv this Add fuses into (BlazeFace
+        // full range's FPN: conv(12^2 features) + Resize(6^2 branch), the conv first in ONNX
+        // order).  The fused step then runs after the shortcut's producer: nothing between reads
+        // the conv's output (its one consumer is this Add), so moving it to the end is safe.
+        if (val(r).step > si) {
+            Step moved = P.steps[si];
+            P.steps.erase(P.steps.begin() + si);
+            P.steps.push_back(std::move(moved));
+            const int last = (int)P.steps.size() - 1;
+            for (auto &kv : vals) {
+                if (kv.second.step == si) kv.second.step = last;
+                else if (kv.second.step > si) kv.second.step--;
+            }
+        }
         return true;
     }
     if (!ensure_tensor(nd.in[0]) || !ensure_tensor(nd.in[1])) return false;
