@@ -32,7 +32,17 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmParams P) {
     const bool valid = j < P.ncols;
     const int jj = valid ? j : 0;
     const int n = jj / P.P, q = jj - n * P.P;
-    const float *xc = P.x + (int64_t)n * P.x_sN + q;
+    const float *xc;
+    // im2col walk of this lane's k = kh, kh + 2, ... as (ci, ky, kx): no per-element division
+    int ci = 0, ky = 0, kx = kh;
+    if constexpr (FULLPLANE) {
+        const int oy = q / P.out_W, ox = q - oy * P.out_W;
+        xc = P.x + (int64_t)n * P.x_sN + (int64_t)oy * P.pk * P.x_W + ox * P.pk;
+        ky = kh / P.pk;
+        kx = kh - ky * P.pk;
+    } else {
+        xc = P.x + (int64_t)n * P.x_sN + q;
+    }
 
     f32x16 acc[MT];
 #pragma unroll
@@ -56,8 +66,14 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmParams P) {
             const int kcl = k < P.K ? k : P.K - 1;
             float v;
             if constexpr (FULLPLANE) {
-                const int ci = kcl / P.KK, kq = kcl - ci * P.KK;
-                v = xc[(int64_t)ci * P.x_sC + (int64_t)kq * P.x_sK];
+                v = xc[k < P.K ? (int64_t)ci * P.x_sC + ky * P.x_W + kx : 0];
+                kx += 2;  // pk >= 2: at most one wrap of kx, then of ky
+                const bool wx = kx >= P.pk;
+                kx -= wx ? P.pk : 0;
+                ky += wx ? 1 : 0;
+                const bool wy = ky >= P.pk;
+                ky -= wy ? P.pk : 0;
+                ci += wy ? 1 : 0;
             } else {
                 v = xc[(int64_t)kcl * P.x_sC];
             }

@@ -435,12 +435,17 @@ bool Compiler::lower_conv(const OnnxNode &nd) {
     const bool pointwise = g == 1 && kh == 1 && kw == 1 && st[0] == 1 && st[1] == 1 &&
                            pads[0] == 0 && pads[1] == 0 && pads[2] == 0 && pads[3] == 0;
     const bool fullplane = g == 1 && kh == H && kw == W && OH == 1 && OW == 1 && pads[0] == 0 &&
-                           pads[1] == 0 && pads[2] == 0 && pads[3] == 0;
+                           pads[1] == 0 && pads[2] == 0 && pads[3] == 0 && (kw >= 2 || kh == 1);
+    // non-overlapping patches (kernel == stride, no padding: FaceMesh V2's 2x2/2 downsampling
+    // convs) are a GEMM over k = (ci, ky, kx) whose B operand gathers each output's patch
+    const bool patch = g == 1 && kh == kw && st[0] == kh && st[1] == kw && kh >= 2 && kh <= 4 &&
+                       pads[0] == 0 && pads[1] == 0 && pads[2] == 0 && pads[3] == 0 &&
+                       H % kh == 0 && W % kw == 0 && !fullplane;
     if (depthwise) {
         s.kind = S_DW;
         s.w_off = push_weights(w->f);
         s.b_off = push_weights(bias);
-    } else if (pointwise || fullplane) {
+    } else if (pointwise || fullplane || patch) {
         s.kind = S_GEMM;
         s.in2 = TRef{};
         s.KK = kh * kw;
@@ -1244,6 +1249,8 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook
             g.x_sC = x.sC;
             g.KK = s.KK;
             g.x_sK = 1;
+            g.pk = s.kw;
+            g.x_W = s.in.W;
             g.P = s.out.H * s.out.W;
             g.ncols = b.N * g.P;
             g.M = s.M;
