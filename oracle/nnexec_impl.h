@@ -420,6 +420,68 @@ static int NN(op_gap)(struct NN(net_s) *n, const NN(node) *nd) {
     return 0;
 }
 
+/* AveragePool (count_include_pad = 0, no ceil_mode): the mean of the in-bounds window */
+static int NN(op_avgpool)(struct NN(net_s) *n, const NN(node) *nd) {
+    NN(tensor) *x = NN(find)(n, nd->in[0]);
+    if (!x) FAIL("missing input");
+    int64_t k[2] = {1, 1}, st[2] = {1, 1}, pads[4] = {0, 0, 0, 0};
+    NN(attr_ints)(nd, "kernel_shape", k, 2);
+    NN(attr_ints)(nd, "strides", st, 2);
+    NN(attr_ints)(nd, "pads", pads, 4);
+    if (NN(attr_i)(nd, "ceil_mode", 0)) FAIL("AveragePool ceil_mode unsupported");
+    int64_t C = x->dims[1], H = x->dims[2], W = x->dims[3];
+    int64_t OH = (H + pads[0] + pads[2] - k[0]) / st[0] + 1;
+    int64_t OW = (W + pads[1] + pads[3] - k[1]) / st[1] + 1;
+    int64_t od[4] = {1, C, OH, OW};
+    NN(tensor) *y = NN(new_out)(n, nd->out[0], 4, od);
+    for (int64_t c = 0; c < C; c++)
+        for (int64_t oy = 0; oy < OH; oy++)
+            for (int64_t ox = 0; ox < OW; ox++) {
+                REAL s = 0;
+                int64_t cnt = 0;
+                for (int64_t ky = 0; ky < k[0]; ky++)
+                    for (int64_t kx = 0; kx < k[1]; kx++) {
+                        int64_t iy = oy * st[0] - pads[0] + ky, ix = ox * st[1] - pads[1] + kx;
+                        if (iy < 0 || iy >= H || ix < 0 || ix >= W) continue;
+                        s += x->f[(c * H + iy) * W + ix];
+                        cnt++;
+                    }
+                y->f[(c * OH + oy) * OW + ox] = s / (REAL)cnt;
+            }
+    return 0;
+}
+
+/* ReduceMean over a set of trailing axes (opset <= 17: axes attribute) */
+static int NN(op_reducemean)(struct NN(net_s) *n, const NN(node) *nd) {
+    NN(tensor) *x = NN(find)(n, nd->in[0]);
+    if (!x) FAIL("missing input");
+    int64_t axes[6];
+    int na = NN(attr_ints)(nd, "axes", axes, 6);
+    if (na <= 0) FAIL("ReduceMean needs axes");
+    int keep = (int)NN(attr_i)(nd, "keepdims", 1);
+    int red[6] = {0};
+    for (int i = 0; i < na; i++) red[axes[i] < 0 ? axes[i] + x->ndim : axes[i]] = 1;
+    /* outer = dims before the first reduced axis (reduced axes must be trailing) */
+    int first = x->ndim;
+    for (int i = 0; i < x->ndim; i++)
+        if (red[i]) { first = i; break; }
+    for (int i = first; i < x->ndim; i++)
+        if (!red[i]) FAIL("ReduceMean over non-trailing axes unsupported");
+    int64_t outer = 1, inner = 1, od[6];
+    int nd_out = 0;
+    for (int i = 0; i < x->ndim; i++) {
+        if (i < first) { outer *= x->dims[i]; od[nd_out++] = x->dims[i]; }
+        else { inner *= x->dims[i]; if (keep) od[nd_out++] = 1; }
+    }
+    NN(tensor) *y = NN(new_out)(n, nd->out[0], nd_out, od);
+    for (int64_t o = 0; o < outer; o++) {
+        REAL s = 0;
+        for (int64_t i = 0; i < inner; i++) s += x->f[o * inner + i];
+        y->f[o] = s / (REAL)inner;
+    }
+    return 0;
+}
+
 static int NN(op_gemm)(struct NN(net_s) *n, const NN(node) *nd) {
     NN(tensor) *a = NN(find)(n, nd->in[0]), *b = NN(find)(n, nd->in[1]);
     NN(tensor) *c = nd->nin > 2 ? NN(find)(n, nd->in[2]) : NULL;
@@ -461,6 +523,8 @@ static int NN(exec_node)(struct NN(net_s) *n, const NN(node) *nd) {
     if (!strcmp(op, "Concat")) return NN(op_concat)(n, nd);
     if (!strcmp(op, "GlobalAveragePool")) return NN(op_gap)(n, nd);
     if (!strcmp(op, "Gemm")) return NN(op_gemm)(n, nd);
+    if (!strcmp(op, "AveragePool")) return NN(op_avgpool)(n, nd);
+    if (!strcmp(op, "ReduceMean")) return NN(op_reducemean)(n, nd);
     snprintf(g_err, sizeof(g_err), "unsupported op %s", op);
     return -1;
 }

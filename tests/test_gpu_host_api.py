@@ -55,6 +55,38 @@ def test_estimator_facemesh(H, golden_dir, kat):
         assert l2 <= 1e-3, l2
 
 
+@pytest.mark.parametrize("net,model,side,lo", [("eye", "iris_landmark", 64, -1.0),
+                                               ("face68_pfld", "landmarks_68_pfld", 112, 0.0),
+                                               ("face68_peppa", "slim_160_latest", 160, -1.0)])
+def test_estimator_eye_and_68_point(H, models_dir, net, model, side, lo):
+    """Estimator over the SURVEY 8(f)-4 networks on a rotated view of a seeded image against the
+    oracle chain: preprocessing, f32 network, extract (eye.rs:47-64: iris first, then the
+    contour; multipie68.rs:71-80: (x, y) * input resolution, z = 0) and the map-out
+    (landmark.rs:336-345)."""
+    import oracle as O
+    rng = np.random.default_rng(21)
+    img = rng.integers(0, 256, size=(150, 210, 4), dtype=np.uint8)
+    est = H.Estimator(net)
+    roi = O.RRect(O.Rect(100.0, 70.0, 120.0, 96.0), 0.25)
+    view = O.view_compose(O.view_full(210, 150), roi)
+    hv = H.ViewData.full(210, 150).view(H.RotatedRect(H.Rect.from_center(100.0, 70.0, 120.0, 96.0), 0.25))
+    r = est.estimate(img, hv)
+    lrect = O.grow_to_fit_aspect(O.Rect.from_top_left(0, 0, view.rect.w, view.rect.h), side, side)
+    x = O.preproc(img, O.view_compose(view, lrect), side, side, lo, 1.0)
+    outs = O.Net(os.path.join(models_dir, model + ".onnx"), f64=False).run(x[None])
+    if net == "eye":
+        pos = np.concatenate([outs[1].reshape(5, 3), outs[0].reshape(71, 3)])
+    else:
+        xy = outs[0].reshape(-1)[:136].reshape(68, 2) * np.float32(side)
+        pos = np.concatenate([xy, np.zeros((68, 1), np.float32)], 1).astype(np.float32)
+    want = O.estimator_map(pos, lrect, side)
+    assert r["landmarks"].shape == want.shape
+    per_px = lrect.w / side
+    l2 = np.sqrt(((r["landmarks"][:, :2] - want[:, :2]) ** 2).sum(-1)).max() / per_px
+    assert l2 <= 1e-3, l2
+    assert r["confidence"] == 1.0  # no Confidence impl in the reference outputs
+
+
 def test_tracker_follows_face(H, golden_dir):
     """LandmarkTracker::track (landmark.rs:463-501): seeded with the whole crop, tracking holds
     and the next ROI stays on the face."""

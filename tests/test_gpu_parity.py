@@ -22,8 +22,13 @@ MODELS = {
     # SURVEY 8(f)-1 (fixtures in next_models.npz)
     "face_detection_full_range": (192, -1.0, 1.0),
     "face_landmarks_detector": (256, -1.0, 1.0),
+    # EyeNetwork and the two 68-point networks
+    "iris_landmark": (64, -1.0, 1.0),
+    "landmarks_68_pfld": (112, 0.0, 1.0),
+    "slim_160_latest": (160, -1.0, 1.0),
 }
-NEXT = ("face_detection_full_range", "face_landmarks_detector")
+NEXT = ("face_detection_full_range", "face_landmarks_detector", "iris_landmark", "landmarks_68_pfld",
+        "slim_160_latest")
 ABS_TOL = 2e-3
 
 
@@ -49,10 +54,16 @@ def test_model_vs_f64_golden(nets, golden_dir, model):
         err = float(np.abs(o - want).max())
         print(f"{model} out{oi}: max|gpu - f64| = {err:.3e}")
         assert err <= ABS_TOL, (model, oi, err)
-    if model in ("face_landmark", "hand_landmark_lite", "face_landmarks_detector"):
+    if model in ("face_landmark", "hand_landmark_lite", "face_landmarks_detector", "iris_landmark"):
         lm = outs[0].reshape(2, -1, 3)
         want = np.stack([g[f"{model}/{k}/out0"].reshape(-1, 3) for k in range(2)])
         l2 = np.sqrt(((lm[..., :2] - want[..., :2]) ** 2).sum(-1)).max()
+        assert l2 <= 1e-3, l2
+    if model in ("landmarks_68_pfld", "slim_160_latest"):
+        # (x, y) relative to the input side (multipie68.rs:71-80): L2 in network pixels
+        lm = outs[0].reshape(2, -1)[:, :136].reshape(2, 68, 2) * s
+        want = np.stack([g[f"{model}/{k}/out0"].reshape(-1)[:136].reshape(68, 2) for k in range(2)]) * s
+        l2 = np.sqrt(((lm - want) ** 2).sum(-1)).max()
         assert l2 <= 1e-3, l2
 
 

@@ -61,7 +61,12 @@ def test_plan_compiles_and_fuses(models_dir, model, launches, chained):
 
 @pytest.mark.parametrize("model,outputs", [
     ("face_detection_full_range", ["reshaped_regressor_face_4", "reshaped_classifier_face_4"]),
-    ("face_landmarks_detector", None)])
+    ("face_landmarks_detector", None),
+    # whole-plane AveragePool / ReduceMean(W, then H) -> GAP, and the channel
+    # Concat of the pooled vectors written in place by their producers
+    ("iris_landmark", ["output_eyes_contours_and_brows", "output_iris"]),
+    ("landmarks_68_pfld", ["output"]),
+    ("slim_160_latest", ["output1"])])
 def test_next_models_compile(models_dir, model, outputs):
     """BlazeFace full range (Resize linear FPN) and FaceMesh V2 (fp16 weights)
     lower to the same fused kernels, with no standalone element-wise pass."""
@@ -190,7 +195,8 @@ def test_malformed_tensor_is_a_model_error(case):
 
 @pytest.mark.parametrize("model", ["face_detection_short_range", "face_landmark", "palm_detection_lite",
                                    "hand_landmark_lite", "face_detection_full_range",
-                                   "face_landmarks_detector"])
+                                   "face_landmarks_detector", "iris_landmark", "landmarks_68_pfld",
+                                   "slim_160_latest"])
 def test_plan_reads_only_produced_tensors(models_dir, model):
     """Every launch reads tensors (its input and its fused shortcut) that an earlier launch wrote.
     BlazeFace full range fuses an FPN Add into a conv that precedes, in ONNX order, the Resize

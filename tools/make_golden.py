@@ -287,6 +287,10 @@ def decode_cases():
 NEXT_SPECS = {  # BlazeFace full range (face/detection.rs:61-94), FaceMesh V2 (mediapipe.rs:81-116)
     "face_detection_full_range": ("face_detection_full_range.onnx", 192, -1.0, 1.0),
     "face_landmarks_detector": ("face_landmarks_detector.onnx", 256, -1.0, 1.0),
+    # face/eye.rs:29-64, face/landmark/multipie68.rs:46-118
+    "iris_landmark": ("iris_landmark.onnx", 64, -1.0, 1.0),
+    "landmarks_68_pfld": ("landmarks_68_pfld.onnx", 112, 0.0, 1.0),
+    "slim_160_latest": ("slim_160_latest.onnx", 160, -1.0, 1.0),
 }
 
 

@@ -52,7 +52,11 @@ LandmarkNetwork landmark_net(const std::string &name) {
     if (name == "facemesh") return LandmarkNetwork::face_mesh_v1();
     if (name == "facemesh_v2") return LandmarkNetwork::face_mesh_v2();
     if (name == "hand") return LandmarkNetwork::hand_lite();
-    throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "landmark network must be 'facemesh', 'facemesh_v2' or 'hand'");
+    if (name == "eye") return LandmarkNetwork::eye();
+    if (name == "face68_pfld") return LandmarkNetwork::face_onnx_68();
+    if (name == "face68_peppa") return LandmarkNetwork::peppa_68();
+    throw ZaruError(ZR_ERR_INVALID_ARGUMENT,
+                    "landmark network must be 'facemesh', 'facemesh_v2', 'hand', 'eye', 'face68_pfld' or 'face68_peppa'");
 }
 
 // Detector::detect_impl after inference on raw outputs (detection.rs:231-267)

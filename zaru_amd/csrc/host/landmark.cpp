@@ -1,14 +1,38 @@
 // landmark.cpp -- see landmark.h.
 #include "landmark.h"
 
+#include <algorithm>
+
 namespace zh {
 
 LandmarkNetwork LandmarkNetwork::face_mesh_v1() { return {NetworkKind::FaceMeshV1, 468}; }
 LandmarkNetwork LandmarkNetwork::face_mesh_v2() { return {NetworkKind::FaceMeshV2, 478}; }
+LandmarkNetwork LandmarkNetwork::eye() { return {NetworkKind::IrisLandmark, 76}; }
+LandmarkNetwork LandmarkNetwork::face_onnx_68() { return {NetworkKind::FaceOnnx68, 68}; }
+LandmarkNetwork LandmarkNetwork::peppa_68() { return {NetworkKind::PeppaFacialLandmark68, 68}; }
 LandmarkNetwork LandmarkNetwork::hand_lite() { return {NetworkKind::HandLandmarkLite, 21}; }
 
-void extract_landmarks(const LandmarkNetwork &net, const float *const *outs, Estimate &e) {
+void extract_landmarks(const LandmarkNetwork &net, const float *const *outs, Estimate &e,
+                       uint32_t in_w, uint32_t in_h) {
     const size_t n = (size_t)net.num_landmarks;
+    if (net.kind == NetworkKind::IrisLandmark) {
+        // iris (5 x 3, output 1) first, then the eye contour (71 x 3, output 0) (eye.rs:47-64)
+        e.positions.resize(3 * n);
+        std::copy(outs[1], outs[1] + 15, e.positions.begin());
+        std::copy(outs[0], outs[0] + 3 * (n - 5), e.positions.begin() + 15);
+        e.confidence = 1.f;
+        return;
+    }
+    if (net.kind == NetworkKind::FaceOnnx68 || net.kind == NetworkKind::PeppaFacialLandmark68) {
+        // (x, y) pairs relative to the input resolution, z = 0 (multipie68.rs:71-80)
+        e.positions.assign(3 * n, 0.f);
+        for (size_t i = 0; i < n; i++) {
+            e.positions[3 * i] = outs[0][2 * i] * (float)in_w;
+            e.positions[3 * i + 1] = outs[0][2 * i + 1] * (float)in_h;
+        }
+        e.confidence = 1.f;
+        return;
+    }
     e.positions.assign(outs[0], outs[0] + 3 * n);
     if (net.kind == NetworkKind::FaceMeshV1) {
         e.confidence = sigmoid(outs[1][0]);  // face_flag, mediapipe.rs:60
@@ -24,6 +48,7 @@ void extract_landmarks(const LandmarkNetwork &net, const float *const *outs, Est
 
 float estimate_angle(const LandmarkNetwork &net, const Estimate &e) {
     if (is_face_mesh(net.kind)) return signed_angle_to(e.xy(263) - e.xy(33), Vec2{1.f, 0.f});
+    if (net.kind != NetworkKind::HandLandmarkLite) return 0.f;
     return signed_angle_to(e.xy(0) - e.xy(9), Vec2{0.f, 1.f});
 }
 
@@ -55,7 +80,7 @@ Estimate &Estimator::estimate(const Image &img, const ViewData &view) {
     auto outs = cnn_->estimate(img, {v});
     std::vector<const float *> ptrs;
     for (auto &o : outs) ptrs.push_back(o.data());
-    extract_landmarks(net_, ptrs.data(), est_);
+    extract_landmarks(net_, ptrs.data(), est_, cnn_->input_width(), cnn_->input_height());
     // the default LandmarkFilter is a no-op (landmark.rs:151-158)
     map_estimate(est_, rect, cnn_->input_width());
     return est_;

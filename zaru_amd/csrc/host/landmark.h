@@ -16,6 +16,9 @@ struct LandmarkNetwork {
     int num_landmarks;  // 468 / 478 / 21
     static LandmarkNetwork face_mesh_v1();
     static LandmarkNetwork face_mesh_v2();  // mediapipe.rs:81-116
+    static LandmarkNetwork eye();           // face/eye.rs:29-64 (76 points: 5 iris + 71 contour)
+    static LandmarkNetwork face_onnx_68();  // multipie68.rs:83-118
+    static LandmarkNetwork peppa_68();      // multipie68.rs:46-81
     static LandmarkNetwork hand_lite();
 };
 
@@ -31,11 +34,17 @@ struct Estimate {
 };
 
 // extract() of each network from one image's raw outputs (mediapipe.rs:59-71,
-// hand/landmark.rs:298-322).  `outs[i]` points at that image's slice of output i.
-void extract_landmarks(const LandmarkNetwork &net, const float *const *outs, Estimate &e);
+// hand/landmark.rs:298-322, eye.rs:47-64, multipie68.rs:71-80,108-117).  `outs[i]` points at
+// that image's slice of output i; in_w / in_h: the network input resolution (the 68-point nets
+// emit coordinates relative to it).  Networks whose reference Output has no Confidence (eye,
+// 68-point) report confidence 1.
+void extract_landmarks(const LandmarkNetwork &net, const float *const *outs, Estimate &e,
+                       uint32_t in_w = 0, uint32_t in_h = 0);
 
 // Estimate::angle_radians: FaceMesh eye corners 33 -> 263 against +X (mediapipe.rs:146-160);
-// hand wrist - middle MCP against +Y (hand/landmark.rs:68-78).
+// hand wrist - middle MCP against +Y (hand/landmark.rs:68-78); none for the eye / 68-point
+// networks (the trait default, landmark.rs:217-219) -- 0, which LandmarkTracker adds exactly as
+// `unwrap_or(0.0)` does (landmark.rs:479).
 float estimate_angle(const LandmarkNetwork &net, const Estimate &e);
 
 // Estimator::estimate_impl map-out (landmark.rs:336-345)

@@ -131,6 +131,18 @@ std::shared_ptr<const Cnn> network_cnn(NetworkKind k, int device) {
         file = "face_landmarks_detector.onnx";
         cm = {-1.f, 1.f};
         break;
+    case NetworkKind::IrisLandmark:  // face/eye.rs:33-46
+        file = "iris_landmark.onnx";
+        cm = {-1.f, 1.f};
+        break;
+    case NetworkKind::FaceOnnx68:  // face/landmark/multipie68.rs:93-106
+        file = "landmarks_68_pfld.onnx";
+        cm = {0.f, 1.f};
+        break;
+    case NetworkKind::PeppaFacialLandmark68:  // face/landmark/multipie68.rs:56-69
+        file = "slim_160_latest.onnx";
+        cm = {-1.f, 1.f};
+        break;
     }
     auto nn = std::make_shared<NeuralNetwork>(read_file(dir + "/" + file), std::vector<uint32_t>{}, device);
     auto cnn = std::make_shared<const Cnn>(nn, cm);

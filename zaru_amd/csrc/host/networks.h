@@ -49,6 +49,9 @@ enum class NetworkKind {
     HandLandmarkLite,
     FaceDetectionFullRange,
     FaceMeshV2,
+    IrisLandmark,            // face::eye::EyeNetwork
+    FaceOnnx68,              // face::landmark::multipie68::FaceOnnx (landmarks_68_pfld)
+    PeppaFacialLandmark68,   // face::landmark::multipie68::PeppaFacialLandmark (slim_160)
 };
 
 inline bool is_face_mesh(NetworkKind k) { return k == NetworkKind::FaceMeshV1 || k == NetworkKind::FaceMeshV2; }

@@ -318,7 +318,7 @@ void DetectTrackPipeline::stage_map(Slot &s) {
         const float *outs[4];
         for (size_t k = 0; k < nout; k++) outs[k] = &s.h_lm[k][i * lc.nn().output_per_image(k)];
         Estimate e;
-        extract_landmarks(cfg_.landmarker, outs, e);
+        extract_landmarks(cfg_.landmarker, outs, e, lin_w, lc.input_height());
         map_estimate(e, s.local_rect[i], lin_w);
         r.confidence = e.confidence;
         r.tracked = tracker_update(cfg_.landmarker, r.roi, r.result.view_rect, cfg_.loss_threshold,

@@ -14,7 +14,8 @@ namespace {
 struct Val {
     std::vector<int64_t> shape;
     int tensor = -1;        // internal storage id when materialised
-    int lazy = 0;           // 1: MaxPool 2x2/2 of lazy_src, 2: channel Pad of lazy_src
+    int lazy = 0;           // 1: MaxPool 2x2/2 of lazy_src, 2: channel Pad of lazy_src,
+                            // 3: ReduceMean over W of lazy_src (completed by the one over H)
     std::string lazy_src;
     int step = -1;          // producing step (after fusion aliasing)
     int consumers = 0;
@@ -185,6 +186,30 @@ bool Compiler::infer_shapes() {
         } else if (op == "GlobalAveragePool") {
             auto &x = in(0);
             s = {x[0], x[1], 1, 1};
+        } else if (op == "AveragePool") {
+            auto &x = in(0);
+            auto k = nd.getints("kernel_shape");
+            auto st = nd.getints("strides", {1, 1});
+            auto pads = nd.getints("pads", {0, 0, 0, 0});
+            if (k.size() != 2 || st.size() != 2 || st[0] <= 0 || st[1] <= 0 || pads.size() != 4 || x.size() != 4 ||
+                k[0] <= 0 || k[1] <= 0 || nd.geti("ceil_mode", 0))
+                return fail("AveragePool kernel_shape/strides/pads");
+            s = {x[0], x[1], (x[2] + pads[0] + pads[2] - k[0]) / st[0] + 1,
+                 (x[3] + pads[1] + pads[3] - k[1]) / st[1] + 1};
+        } else if (op == "ReduceMean") {
+            auto &x = in(0);
+            auto axes = nd.getints("axes");
+            if (axes.empty() && nd.in.size() > 1 && init(nd.in[1])) axes = init(nd.in[1])->i64;
+            const bool keep = nd.geti("keepdims", 1) != 0;
+            if (axes.empty()) return fail("ReduceMean over all axes unsupported");
+            for (size_t i = 0; i < x.size(); i++) {
+                bool red = false;
+                for (auto a : axes)
+                    if (a == (int64_t)i || a + (int64_t)x.size() == (int64_t)i) red = true;
+                if (red && i < 2) return fail("ReduceMean over batch/channels unsupported");
+                if (!red) s.push_back(x[i]);
+                else if (keep) s.push_back(1);
+            }
         } else if (op == "Squeeze") {
             auto &x = in(0);
             auto axes = nd.getints("axes");
@@ -356,6 +381,7 @@ bool Compiler::ensure_tensor(const std::string &name) {
     if (v.is_input || v.tensor >= 0) return true;
     if (v.out_idx >= 0) return fail("graph output " + name + " is also consumed internally");
     if (!v.lazy) return fail("value " + name + " was never materialised");
+    if (v.lazy == 3) return fail("partial ReduceMean " + name + " is consumed by other than its H mean");
     if (!ensure_tensor(v.lazy_src)) return false;
     Step s;
     s.kind = S_ELT;
@@ -734,6 +760,79 @@ bool Compiler::lower() {
             s.bytes = 4.0 * (per_image(xs) + xs[1]);
             P.steps.push_back(s);
             val(nd.out[0]).step = (int)P.steps.size() - 1;
+        } else if (op == "AveragePool" || op == "ReduceMean") {
+            // global average pooling in its two spellings: an AveragePool whose window is the
+            // whole plane (landmarks_68_pfld), and ReduceMean over W then over H (slim_160) or
+            // over both at once.  ReduceMean over W alone stays lazy until the H mean follows.
+            auto &xs = val(nd.in[0]).shape;
+            std::string src = nd.in[0];
+            bool gap = false;
+            if (op == "AveragePool") {
+                auto k = nd.getints("kernel_shape");
+                auto pads = nd.getints("pads", {0, 0, 0, 0});
+                gap = xs.size() == 4 && k.size() == 2 && k[0] == xs[2] && k[1] == xs[3] &&
+                      pads == std::vector<int64_t>{0, 0, 0, 0};
+                if (!gap) return fail("only whole-plane AveragePool is supported");
+            } else {
+                auto axes = nd.getints("axes");
+                if (axes.empty() && nd.in.size() > 1 && init(nd.in[1])) axes = init(nd.in[1])->i64;
+                std::set<int64_t> ax;
+                for (auto a : axes) ax.insert(a < 0 ? a + (int64_t)xs.size() : a);
+                if (xs.size() == 4 && ax == std::set<int64_t>{2, 3}) {
+                    gap = true;
+                } else if (xs.size() == 4 && ax == std::set<int64_t>{3} && nd.geti("keepdims", 1) == 0) {
+                    Val &y = val(nd.out[0]);
+                    y.lazy = 3;
+                    y.lazy_src = nd.in[0];
+                    continue;
+                } else if (xs.size() == 3 && ax == std::set<int64_t>{2} && val(nd.in[0]).lazy == 3) {
+                    src = val(nd.in[0]).lazy_src;  // mean over H of the mean over W
+                    gap = true;
+                } else {
+                    return fail("ReduceMean pattern unsupported (only the spatial mean)");
+                }
+            }
+            if (!gap || !ensure_tensor(src)) return false;
+            auto &ss = val(src).shape;
+            Step s;
+            s.kind = S_GAP;
+            s.name = nd.name.empty() ? nd.out[0] : nd.name;
+            s.in = ref_of(src);
+            s.out = out_ref(nd.out[0], (int)ss[1], 1, 1);
+            s.bytes = 4.0 * (per_image(ss) + ss[1]);
+            P.steps.push_back(s);
+            val(nd.out[0]).step = (int)P.steps.size() - 1;
+        } else if (op == "Concat") {
+            // channel Concat of per-image vectors feeding an internal consumer (the pooled
+            // multi-scale features of the 68-point nets): each member's producing step writes
+            // straight into its channel range of one storage, so no copy runs
+            if (nd.geti("axis", 0) != 1 && nd.geti("axis", 0) != -(int64_t)val(nd.out[0]).shape.size() + 1)
+                return fail("internal Concat on axis != 1 unsupported");
+            auto &ys = val(nd.out[0]).shape;
+            if (per_image(ys) != ys[1]) return fail("internal Concat of non-vector tensors unsupported");
+            if (val(nd.out[0]).out_idx >= 0) return fail("unexpected output placement on Concat");
+            const int id = new_storage(ys[1]);
+            int c0 = 0;
+            for (auto &in_name : nd.in) {
+                if (!ensure_tensor(in_name)) return false;
+                Val &x = val(in_name);
+                const int C = (int)per_image(x.shape);
+                if (x.consumers != 1 || x.is_input || x.tensor < 0) return fail("Concat member " + in_name + " is shared");
+                Step *prod = nullptr;
+                for (auto &st : P.steps)
+                    if (st.out.kind == 0 && st.out.id == x.tensor) prod = &st;
+                if (!prod || prod->kind == S_CHAIN || prod->out.C * prod->out.H * prod->out.W != C)
+                    return fail("Concat member " + in_name + " has no retargetable producer");
+                for (auto &st : P.steps)
+                    if ((st.in.kind == 0 && st.in.id == x.tensor) || (st.in2.kind == 0 && st.in2.id == x.tensor))
+                        return fail("Concat member " + in_name + " is read internally");
+                prod->out.id = id;
+                prod->out.c_off = c0;
+                c0 += C;
+            }
+            Val &y = val(nd.out[0]);
+            y.tensor = id;
+            y.step = -1;
         } else if (op == "Squeeze" || op == "Reshape" || op == "Flatten") {
             // internal alias: same storage, reinterpreted as (C = per-image size, 1, 1) or kept
             if (!ensure_tensor(nd.in[0])) return false;
@@ -1193,7 +1292,7 @@ Resolved resolve(const TRef &r, const Plan &plan, const Binding &b) {
     Resolved o{};
     const int64_t P = (int64_t)r.H * r.W;
     if (r.kind == 0) {
-        o.p = b.arena + plan.storage_off[r.id] * b.N;
+        o.p = b.arena + plan.storage_off[r.id] * b.N + (int64_t)r.c_off * P * b.N;
         o.sN = P;
         o.sC = P * b.N;
         o.sP = 1;

@@ -26,6 +26,8 @@ struct TRef {
     int C = 0, H = 1, W = 1;
     // kind 2: element (n, c, q) -> out[id] + n*o_sN + off + c*o_sC + q*o_sP
     int64_t off = 0, o_sN = 0, o_sC = 0, o_sP = 1;
+    // kind 0: first channel inside the storage (a member of an internal channel Concat)
+    int c_off = 0;
 };
 
 struct ActDesc {
