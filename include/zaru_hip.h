@@ -104,6 +104,57 @@ int zr_detection_candidates_async(const float *d_logits, const float *d_boxes, u
                                   uint32_t anchors, uint32_t params, float logit_min,
                                   uint32_t cap, int32_t *d_count, float *d_rec, void *hip_stream);
 
+/* ---- LandmarkTracker state on the device ------------------------------
+ * A video loop of LandmarkTracker::track (crates/zaru/src/landmark.rs:463-501) over n streams
+ * without a host round trip per frame: the tracker state lives in HBM, the landmark network
+ * samples views that the previous update wrote (zr_cnn_estimate_device_views_async), and
+ * zr_track_update_async consumes that estimate: loss check, map-out, angle, transform_out,
+ * RotatedRect::bounding, grow_rel(padding), and the next view.  ROI i is evaluated on frame i
+ * of each step's frame array.  Geometry follows the host restatement operation for operation
+ * (f32, no contraction); cos/sin/atan2/exp are the device's (<= 2 ulp from glibc), so results
+ * match the host path within tolerance, not bit for bit. */
+typedef struct {
+    float roi[5];       /* RotatedRect {cx, cy, w, h, rad} tracked next (LandmarkTracker::roi) */
+    float view_rect[5]; /* roi.grow_to_fit_aspect(aspect) of the pending estimate */
+    float local[3];     /* Estimator map-out rect of that estimate: x, y, w */
+    uint32_t active;    /* 0 once lost (roi = None) */
+    uint32_t frame_w, frame_h;
+    uint32_t tracked;   /* last step: 1 tracked, 0 lost / inactive */
+    float confidence;   /* last step's Confidence::confidence */
+    float updated[5];   /* last step's updated_roi */
+} zr_track_state;
+
+/* One view of the preprocessing's view table (the sampling parameters of a zr_view). */
+typedef struct {
+    float half_w, half_h, tl_x, tl_y, view_w, view_h, cos_r, sin_r;
+    uint32_t frame, pad;
+} zr_view_desc;
+
+typedef struct {
+    int kind;           /* 0 FaceMesh V1/V2 (face_flag = sigmoid(out1), eyes 33->263 vs +X),
+                           1 hand (presence = out1, wrist 0 -> MCP 9 vs +Y),
+                           2 no confidence / angle (EyeNetwork), 3 as 2 with relative (x, y)
+                           pairs (68-point networks) */
+    int num_landmarks;
+    int in_w, in_h;     /* network input */
+    int aspect_w, aspect_h;
+    float loss_thresh, padding;
+} zr_track_cfg;
+
+/* Derive every state's first view from state.roi (LandmarkTracker::set_roi); no estimate. */
+int zr_track_seed_async(zr_track_state *d_state, size_t n, const zr_track_cfg *cfg,
+                        zr_view_desc *d_views, void *hip_stream);
+/* Consume the estimate made on d_views (landmark output 0, and output 1 with flag_stride floats
+ * per image for kinds 0/1), update the states, write frame-space landmarks to d_lm_out
+ * (n x L x 3, may be NULL) and the next views. */
+int zr_track_update_async(zr_track_state *d_state, size_t n, const zr_track_cfg *cfg,
+                          const float *d_landmarks, const float *d_flag, size_t flag_stride,
+                          float *d_lm_out, zr_view_desc *d_views, void *hip_stream);
+/* Cnn::estimate (nn/mod.rs:118-126) with a device-resident view table (frames: host array). */
+int zr_cnn_estimate_device_views_async(zr_session *s, const zr_frame *frames, size_t n_frames,
+                                       const zr_view_desc *d_views, size_t n_views, float lo,
+                                       float hi, float *const *d_outputs, void *hip_stream);
+
 /* Roofline accounting of the compiled plan: algorithmic bytes and FLOPs per image, number
  * of kernel launches per run. */
 int zr_session_stats(const zr_session *s, double *bytes_per_image, double *flops_per_image,

@@ -50,6 +50,9 @@ SIGNATURES = [
     ("zr_cnn_estimate_views_async", _I, [_P, _P, _SZ, _P, _P, _SZ, _F, _F, _P, _P]),
     ("zr_preprocess_views_async", _I, [_P, _SZ, _P, _P, _SZ, _U32, _U32, _F, _F, _P, _P]),
     ("zr_detection_candidates_async", _I, [_P, _P, _U32, _U32, _U32, _F, _U32, _P, _P, _P]),
+    ("zr_track_seed_async", _I, [_P, _SZ, _P, _P, _P]),
+    ("zr_track_update_async", _I, [_P, _SZ, _P, _P, _P, _SZ, _P, _P, _P]),
+    ("zr_cnn_estimate_device_views_async", _I, [_P, _P, _SZ, _P, _SZ, _F, _F, _P, _P]),
     ("zr_session_stats", _I, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(_SZ)]),
     ("zr_plan_describe", _I, [_P, _SZ, _P, _SZ, _P, _SZ, C.POINTER(_SZ)]),
     ("zr_profile_enable", _I, [_P, _I]),

@@ -9,6 +9,7 @@
 #include "hand_tracker.h"
 #include "landmark.h"
 #include "pipeline.h"
+#include "device_tracker.h"
 
 namespace py = pybind11;
 using namespace zh;
@@ -281,6 +282,58 @@ PYBIND11_MODULE(_zaru_host, m) {
         .def("num_tracked", &HandTracker::num_tracked)
         .def_static("filter_detections", &HandTracker::filter_detections)
         .def_static("dedupe_rois", &HandTracker::dedupe_rois);
+
+    // LandmarkTracker state on the device over n video streams
+    py::class_<DeviceTracker>(m, "DeviceTracker")
+        .def(py::init([](const std::string &net, int device, float padding, float loss) {
+                 return new DeviceTracker(landmark_net(net), device, padding, loss);
+             }), py::arg("network") = "facemesh", py::arg("device") = 0,
+             py::arg("padding") = LandmarkTracker::DEFAULT_ROI_PADDING,
+             py::arg("loss_threshold") = LandmarkTracker::DEFAULT_LOSS_THRESHOLD)
+        .def("set_rois", [](DeviceTracker &t, const std::vector<std::tuple<float, float, float, float, float>> &rois,
+                            const std::vector<std::pair<uint32_t, uint32_t>> &sizes) {
+            std::vector<RotatedRect> r;
+            for (auto &v : rois)
+                r.emplace_back(Rect::from_center(std::get<0>(v), std::get<1>(v), std::get<2>(v), std::get<3>(v)),
+                               std::get<4>(v));
+            t.set_rois(r, sizes);
+        })
+        .def("step", [](DeviceTracker &t, const std::vector<std::tuple<uint64_t, uint32_t, uint32_t, uint64_t>> &frames) {
+            std::vector<Image> im;
+            for (auto &f : frames) {
+                Image i;
+                i.rgba = reinterpret_cast<const uint8_t *>(std::get<0>(f));
+                i.width = std::get<1>(f);
+                i.height = std::get<2>(f);
+                i.row_stride = std::get<3>(f);
+                i.on_device = true;
+                im.push_back(i);
+            }
+            py::gil_scoped_release nogil;
+            t.step(im);
+        })
+        .def("synchronize", &DeviceTracker::synchronize, py::call_guard<py::gil_scoped_release>())
+        .def("__len__", &DeviceTracker::size)
+        .def("states", [](DeviceTracker &t) {
+            py::list out;
+            for (const auto &s : t.states()) {
+                py::dict d;
+                d["roi"] = RotatedRect(Rect::from_center(s.roi[0], s.roi[1], s.roi[2], s.roi[3]), s.roi[4]);
+                d["updated_roi"] = RotatedRect(Rect::from_center(s.updated[0], s.updated[1], s.updated[2], s.updated[3]), s.updated[4]);
+                d["view_rect"] = RotatedRect(Rect::from_center(s.view_rect[0], s.view_rect[1], s.view_rect[2], s.view_rect[3]), s.view_rect[4]);
+                d["active"] = s.active != 0;
+                d["tracked"] = s.tracked != 0;
+                d["confidence"] = s.confidence;
+                out.append(d);
+            }
+            return out;
+        })
+        .def("landmarks", [](DeviceTracker &t) {
+            auto v = t.landmarks();
+            py::array_t<float> a({(py::ssize_t)t.size(), (py::ssize_t)t.network().num_landmarks, (py::ssize_t)3});
+            std::memcpy(a.mutable_data(), v.data(), v.size() * 4);
+            return a;
+        });
 
     py::class_<DetectTrackPipeline>(m, "DetectTrackPipeline")
         .def(py::init([](const std::string &kind, int device, int threads, uint32_t max_rois,

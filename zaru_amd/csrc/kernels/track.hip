@@ -1,0 +1,228 @@
+// track.hip -- LandmarkTracker::track_impl (crates/zaru/src/landmark.rs:463-501) on the device,
+// so a video loop runs estimate -> update -> next view without a host round trip per frame
+// (SURVEY.md §8f-3).  One workgroup per tracked ROI:
+//   1. Confidence::confidence of the estimate and the loss check (landmark.rs:468-477);
+//   2. Estimator map-out of the landmarks (landmark.rs:336-345) and the estimate angle
+//      (mediapipe.rs:146-160 / hand/landmark.rs:68-78);
+//   3. transform_out into the frame (landmark.rs:481-486) and RotatedRect::bounding at the
+//      tracked angle (rect.rs:287-325): a block min/max reduction;
+//   4. next RoI = grow_rel(padding) (landmark.rs:493), and from it the next estimate's view
+//      exactly as the host builds it (grow_to_fit_aspect, ViewData::view twice,
+//      image/mod.rs:201-210, nn/mod.rs:118-126), written as the preprocessing's view table.
+// f32 throughout, no contraction (HIPFLAGS -ffp-contract=off), Rust's operation order; the only
+// departures from the host restatement are the device cosf / sinf / atan2f / expf (<= 2 ulp).
+#include "../runtime/zr_track.h"
+
+namespace zr {
+namespace {
+
+struct V2 {
+    float x, y;
+};
+struct RRect {  // Rect as (centre, size) (rect.rs:15-18) + rotation
+    float cx, cy, w, h, rad;
+};
+
+__device__ __forceinline__ V2 rot_ccw(V2 v, float r) {  // matrix.rs:571-579, ops.rs:68-77
+    const float c = cosf(r), s = sinf(r), ns = -s;
+    return {(0.f + c * v.x) + ns * v.y, (0.f + s * v.x) + c * v.y};
+}
+
+__device__ __forceinline__ float signed_angle_to(V2 a, V2 b) {  // vector.rs:568-573
+    const float perp = a.x * b.y - a.y * b.x;
+    const float dot = (0.f + a.x * b.x) + a.y * b.y;
+    return -atan2f(perp, dot);
+}
+
+__device__ __forceinline__ RRect from_top_left(float x, float y, float w, float h, float rad) {
+    return {x + w * 0.5f, y + h * 0.5f, w, h, rad};
+}
+
+__device__ __forceinline__ V2 top_left(const RRect &r) { return {r.cx - r.w * 0.5f, r.cy - r.h * 0.5f}; }
+
+__device__ __forceinline__ RRect grow_to_fit_aspect(RRect r, int aw, int ah) {  // rect.rs:104-117
+    const float a = (float)aw / (float)ah;
+    const float tw = r.h * a;
+    if (tw >= r.w) {
+        r.w += tw - r.w;
+    } else {
+        const float th = r.w / a;
+        r.h += th - r.h;
+    }
+    return r;
+}
+
+__device__ __forceinline__ V2 transform_out(const RRect &r, V2 p) {  // rect.rs:417-423
+    const V2 half = {r.w * 0.5f, r.h * 0.5f};
+    const V2 q = rot_ccw({p.x - half.x, p.y - half.y}, r.rad);
+    const V2 tl = top_left(r);
+    return {q.x + half.x + tl.x, q.y + half.y + tl.y};
+}
+
+// ViewData::view (image/mod.rs:201-210): child in the parent's local coordinates
+__device__ __forceinline__ RRect view_of(const RRect &parent, const RRect &child) {
+    const float rad = parent.rad + child.rad;
+    const V2 c = transform_out(parent, {child.cx, child.cy});
+    return from_top_left(c.x - child.w * 0.5f, c.y - child.h * 0.5f, child.w, child.h, rad);
+}
+
+// The next estimate's sampling view of a RoI: track_impl's view_rect + Estimator's aspect-fit
+// local rect (pipeline.cpp stage_decode_and_rois, landmark.rs:465-467 + 320-323).
+__device__ void next_view(TrackState &st, ViewDesc &vd, int frame, int aw, int ah) {
+    const RRect roi = {st.roi[0], st.roi[1], st.roi[2], st.roi[3], st.roi[4]};
+    const RRect vr = grow_to_fit_aspect(roi, aw, ah);
+    const RRect full = from_top_left(0.f, 0.f, (float)st.frame_w, (float)st.frame_h, 0.f);
+    const RRect view = view_of(full, vr);
+    const RRect local = grow_to_fit_aspect(from_top_left(0.f, 0.f, view.w, view.h, 0.f), aw, ah);
+    const RRect net = view_of(view, local);
+    st.view_rect[0] = vr.cx;
+    st.view_rect[1] = vr.cy;
+    st.view_rect[2] = vr.w;
+    st.view_rect[3] = vr.h;
+    st.view_rect[4] = vr.rad;
+    const V2 ltl = top_left(local);
+    st.local[0] = ltl.x;
+    st.local[1] = ltl.y;
+    st.local[2] = local.w;
+    // make_view (session.cpp) on the zr_view {centre, size, rad} of `net`
+    vd.half_w = net.w * 0.5f;
+    vd.half_h = net.h * 0.5f;
+    vd.tl_x = net.cx - net.w * 0.5f;
+    vd.tl_y = net.cy - net.h * 0.5f;
+    vd.view_w = net.w;
+    vd.view_h = net.h;
+    vd.cos_r = cosf(net.rad);
+    vd.sin_r = sinf(net.rad);
+    vd.frame = (uint32_t)frame;
+    vd.pad_ = 0;
+}
+
+__device__ __forceinline__ float wave_min(float v) {
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+
+__global__ __launch_bounds__(256) void track_kernel(const TrackParams P) {
+    const int i = blockIdx.x, tid = threadIdx.x;
+    if (i >= P.n) return;  // whole workgroup
+    __shared__ float red[4][4];
+    TrackState st = P.state[i];
+    if (!P.seed) {
+        if (!st.active) {  // lost earlier: stays lost (roi = None)
+            if (tid == 0) P.state[i].tracked = 0;
+            return;
+        }
+        float conf = 1.f;
+        if (P.kind == 0) conf = 1.f / (1.f + expf(-P.flag[(int64_t)i * P.flag_stride]));  // num.rs:6-8
+        else if (P.kind == 1) conf = P.flag[(int64_t)i * P.flag_stride];
+        if (conf < P.loss_thresh) {
+            if (tid == 0) {
+                P.state[i].active = 0;
+                P.state[i].tracked = 0;
+                P.state[i].confidence = conf;
+            }
+            return;
+        }
+        const int L = P.L;
+        const float *lm = P.lm + (int64_t)i * L * (P.kind == 3 ? 2 : 3);
+        const float scale = st.local[2] / (float)P.in_w;
+        // map-out of landmark j (Estimator, landmark.rs:336-345): p * scale, then + rect.x / .y
+        auto mapped = [&](int j, float &x, float &y, float &z) {
+            if (P.kind == 3) {  // multipie68.rs:71-80: relative (x, y) * input resolution, z = 0
+                x = lm[2 * j] * (float)P.in_w;
+                y = lm[2 * j + 1] * (float)P.in_h;
+                z = 0.f;
+            } else {
+                x = lm[3 * j];
+                y = lm[3 * j + 1];
+                z = lm[3 * j + 2];
+            }
+            x = x * scale;
+            y = y * scale;
+            z = z * scale;
+            x += st.local[0];
+            y += st.local[1];
+        };
+        float est = 0.f;  // Estimate::angle_radians; None -> unwrap_or(0.0) (landmark.rs:479)
+        if (P.kind == 0 || P.kind == 1) {
+            const int a = P.kind == 0 ? 263 : 0, b = P.kind == 0 ? 33 : 9;
+            float ax, ay, az, bx, by, bz;
+            mapped(a, ax, ay, az);
+            mapped(b, bx, by, bz);
+            est = P.kind == 0 ? signed_angle_to({ax - bx, ay - by}, {1.f, 0.f})
+                              : signed_angle_to({ax - bx, ay - by}, {0.f, 1.f});
+        }
+        const float angle = st.roi[4] + est;
+        const RRect vr = {st.view_rect[0], st.view_rect[1], st.view_rect[2], st.view_rect[3], st.view_rect[4]};
+        const float c = cosf(-angle), s = sinf(-angle), ns = -s;  // rect.rs:287-325
+        float mnx = 3.40282347e38f, mny = 3.40282347e38f, mxx = -3.40282347e38f, mxy = -3.40282347e38f;
+        for (int j = tid; j < L; j += 256) {
+            float x, y, z;
+            mapped(j, x, y, z);
+            const V2 o = transform_out(vr, {x, y});
+            if (P.lm_out) {
+                float *q = P.lm_out + ((int64_t)i * L + j) * 3;
+                q[0] = o.x;
+                q[1] = o.y;
+                q[2] = z;
+            }
+            const float rx = (0.f + c * o.x) + ns * o.y, ry = (0.f + s * o.x) + c * o.y;
+            mnx = fminf(mnx, rx);
+            mny = fminf(mny, ry);
+            mxx = fmaxf(mxx, rx);
+            mxy = fmaxf(mxy, ry);
+        }
+        mnx = wave_min(mnx);
+        mny = wave_min(mny);
+        mxx = wave_max(mxx);
+        mxy = wave_max(mxy);
+        const int w = tid >> 6;
+        if ((tid & 63) == 0) {
+            red[w][0] = mnx;
+            red[w][1] = mny;
+            red[w][2] = mxx;
+            red[w][3] = mxy;
+        }
+        __syncthreads();
+        if (tid != 0) return;
+        for (int k = 1; k < 4; ++k) {
+            red[0][0] = fminf(red[0][0], red[k][0]);
+            red[0][1] = fminf(red[0][1], red[k][1]);
+            red[0][2] = fmaxf(red[0][2], red[k][2]);
+            red[0][3] = fmaxf(red[0][3], red[k][3]);
+        }
+        const V2 ctr = rot_ccw({(red[0][0] + red[0][2]) * 0.5f, (red[0][1] + red[0][3]) * 0.5f}, angle);
+        const float uw = red[0][2] - red[0][0], uh = red[0][3] - red[0][1];
+        st.updated[0] = ctr.x;
+        st.updated[1] = ctr.y;
+        st.updated[2] = uw;
+        st.updated[3] = uh;
+        st.updated[4] = angle;
+        // grow_rel(padding) adds padding * size to each side (rect.rs:84-93)
+        const float l = uw * P.padding, t = uh * P.padding;
+        st.roi[0] = ctr.x;
+        st.roi[1] = ctr.y;
+        st.roi[2] = uw + l + l;
+        st.roi[3] = uh + t + t;
+        st.roi[4] = angle;
+        st.tracked = 1;
+        st.confidence = conf;
+    } else if (tid != 0) {
+        return;
+    }
+    next_view(st, P.views[i], i, P.asp_w, P.asp_h);
+    P.state[i] = st;
+}
+
+}  // namespace
+
+const char *launch_track(const TrackParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(track_kernel, dim3(p.n), dim3(256), 0, s, p);
+    return "track_kernel";
+}
+
+}  // namespace zr

@@ -16,6 +16,7 @@
 #include "../../../include/zaru_hip.h"
 #include "onnx_model.h"
 #include "plan.h"
+#include "zr_track.h"
 
 namespace {
 
@@ -524,15 +525,16 @@ int zr_session_run(zr_session *s, size_t batch, const float *const *inputs, size
 
 static int views_common(zr_session *s, Ctx *c, const zr_frame *frames, size_t nf, const zr_view *views,
                         const uint32_t *view_frame, size_t nv, float lo, float hi, float *const *outs,
-                        hipStream_t stream) {
+                        hipStream_t stream, const zr::ViewDesc *d_views = nullptr) {
     const int64_t hw = (int64_t)s->plan.in_H * s->plan.in_W;
     if (s->plan.in_C != 3) return set_err(ZR_ERR_SHAPE, "view sampling needs a 3-channel input");
     if (!(hi > lo)) return set_err(ZR_ERR_INVALID_ARGUMENT, "ColorMapper range must satisfy end > start");
     HIP_TRY(hipStreamWaitEvent(stream, c->done, 0));
-    if (int rc = upload_views(c, frames, nf, views, view_frame, nv, stream)) return rc;
+    // a device view table (the tracker's) needs only the frame table uploaded
+    if (int rc = upload_views(c, frames, nf, views, view_frame, d_views ? 0 : nv, stream)) return rc;
     zr::PreprocParams p{};
     p.frames = c->frames;
-    p.views = c->views;
+    p.views = d_views ? d_views : c->views;
     p.nviews = (int)nv;
     p.OW = s->plan.in_W;
     p.OH = s->plan.in_H;
@@ -570,6 +572,78 @@ int zr_cnn_estimate_views_async(zr_session *s, const zr_frame *frames, size_t n_
         HIP_TRY(hipSetDevice(s->device));
         return views_common(s, c, frames, n_frames, views, view_frame, n_views, lo, hi, d_outputs,
                             (hipStream_t)hip_stream);
+    });
+}
+
+// ---- device-resident tracker state (kernels/track.hip)
+static_assert(sizeof(zr_track_state) == sizeof(zr::TrackState), "zr_track_state layout");
+static_assert(sizeof(zr_view_desc) == sizeof(zr::ViewDesc), "zr_view_desc layout");
+
+static int track_params(zr::TrackParams &p, zr_track_state *d_state, size_t n, const zr_track_cfg *cfg,
+                        zr_view_desc *d_views) {
+    if (!d_state || !cfg || !d_views || n == 0) return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument or n == 0");
+    if (cfg->kind < 0 || cfg->kind > 3 || cfg->num_landmarks <= 0 || cfg->in_w <= 0 || cfg->in_h <= 0 ||
+        cfg->aspect_w <= 0 || cfg->aspect_h <= 0 || !(cfg->padding >= 0.f) || n > (1u << 24))
+        return set_err(ZR_ERR_INVALID_ARGUMENT, "bad tracker configuration");
+    if ((cfg->kind == 0 && cfg->num_landmarks <= 263) || (cfg->kind == 1 && cfg->num_landmarks <= 9))
+        return set_err(ZR_ERR_INVALID_ARGUMENT, "angle landmarks out of range");
+    p.state = reinterpret_cast<zr::TrackState *>(d_state);
+    p.views = reinterpret_cast<zr::ViewDesc *>(d_views);
+    p.n = (int)n;
+    p.L = cfg->num_landmarks;
+    p.kind = cfg->kind;
+    p.in_w = cfg->in_w;
+    p.in_h = cfg->in_h;
+    p.asp_w = cfg->aspect_w;
+    p.asp_h = cfg->aspect_h;
+    p.loss_thresh = cfg->loss_thresh;
+    p.padding = cfg->padding;
+    return ZR_OK;
+}
+
+int zr_track_seed_async(zr_track_state *d_state, size_t n, const zr_track_cfg *cfg, zr_view_desc *d_views,
+                        void *hip_stream) {
+    return guarded([&]() -> int {
+        zr::TrackParams p{};
+        if (int rc = track_params(p, d_state, n, cfg, d_views)) return rc;
+        p.seed = 1;
+        zr::launch_track(p, (hipStream_t)hip_stream);
+        HIP_TRY(hipGetLastError());
+        return ZR_OK;
+    });
+}
+
+int zr_track_update_async(zr_track_state *d_state, size_t n, const zr_track_cfg *cfg, const float *d_landmarks,
+                          const float *d_flag, size_t flag_stride, float *d_lm_out, zr_view_desc *d_views,
+                          void *hip_stream) {
+    return guarded([&]() -> int {
+        zr::TrackParams p{};
+        if (int rc = track_params(p, d_state, n, cfg, d_views)) return rc;
+        if (!d_landmarks || ((cfg->kind == 0 || cfg->kind == 1) && (!d_flag || flag_stride == 0)))
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "missing landmark / flag outputs");
+        p.lm = d_landmarks;
+        p.flag = d_flag;
+        p.flag_stride = (int)flag_stride;
+        p.lm_out = d_lm_out;
+        zr::launch_track(p, (hipStream_t)hip_stream);
+        HIP_TRY(hipGetLastError());
+        return ZR_OK;
+    });
+}
+
+int zr_cnn_estimate_device_views_async(zr_session *s, const zr_frame *frames, size_t n_frames,
+                                       const zr_view_desc *d_views, size_t n_views, float lo, float hi,
+                                       float *const *d_outputs, void *hip_stream) {
+    return guarded([&]() -> int {
+        if (int rc = check_session(s)) return rc;
+        if (!frames || !d_views || !d_outputs || n_views == 0 || n_frames == 0)
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument or no views");
+        Ctx *c = s->acquire();
+        if (!c) return set_err(ZR_ERR_DEVICE, "cannot create execution context");
+        CtxLock lk(c);
+        HIP_TRY(hipSetDevice(s->device));
+        return views_common(s, c, frames, n_frames, nullptr, nullptr, n_views, lo, hi, d_outputs,
+                            (hipStream_t)hip_stream, reinterpret_cast<const zr::ViewDesc *>(d_views));
     });
 }
 

@@ -1,0 +1,42 @@
+// zr_track.h -- device-resident LandmarkTracker state shared by the track
+// kernels (kernels/track.hip) and the runtime (session.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "zr_kernels.h"
+
+namespace zr {
+
+// One tracked ROI (LandmarkTracker, crates/zaru/src/landmark.rs:354-501) kept in HBM between
+// frames: the RoI the next estimate samples, the view geometry that estimate used (for the
+// map-out) and the last result.  Layout mirrored by zr_track_state in include/zaru_hip.h.
+struct TrackState {
+    float roi[5];          // RotatedRect (cx, cy, w, h, rad) tracked next
+    float view_rect[5];    // roi.grow_to_fit_aspect(aspect) of the pending estimate (landmark.rs:465)
+    float local[3];        // Estimator map-out rect of that estimate: x, y (top left), w (landmark.rs:320-345)
+    uint32_t active;       // 0 once lost (the reference sets roi = None, landmark.rs:475)
+    uint32_t frame_w, frame_h;
+    uint32_t tracked;      // last step: 1 tracked, 0 lost (or inactive)
+    float confidence;      // last step's Confidence::confidence
+    float updated[5];      // last step's updated_roi (RotatedRect::bounding, landmark.rs:488-491)
+};
+
+struct TrackParams {
+    TrackState *state;
+    ViewDesc *views;       // out: the next estimate's sampling view per ROI (the preprocessing input)
+    const float *lm;       // landmark output 0 of the last estimate: n x L x 3 (n x 2L for kind 3)
+    const float *flag;     // output 1: n x flag_stride (face_flag logit / presence); null: kind 2/3
+    float *lm_out;         // out: frame-space landmarks, n x L x 3 (may be null)
+    int n, L, flag_stride;
+    int kind;              // 0 FaceMesh (sigmoid flag, eyes 33->263 vs +X), 1 hand (presence, 0->9 vs +Y),
+                           // 2 no confidence / no angle (eye), 3 as 2 with (x, y) relative pairs (68-point)
+    int in_w, in_h;        // network input (map-out scale, kind 3 coordinate scale)
+    int asp_w, asp_h;      // network aspect ratio, reduced
+    float loss_thresh, padding;
+    int seed;              // 1: only derive views from state.roi (no estimate to consume)
+};
+
+const char *launch_track(const TrackParams &p, hipStream_t s);
+
+}  // namespace zr
