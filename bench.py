@@ -92,6 +92,9 @@ def parse():
     ap.add_argument("--no-next", action="store_true",
                     help="skip the SURVEY §8f-1 line (full range + FaceMesh V2) at N = 1")
     ap.add_argument("--next-steps", type=int, default=30)
+    ap.add_argument("--no-tracking", action="store_true",
+                    help="skip the SURVEY §8f-3 device-tracker line at N = 1")
+    ap.add_argument("--tracking-steps", type=int, default=50)
     ap.add_argument("--next-batch", type=int, default=512)
     return ap.parse_args()
 
@@ -186,7 +189,7 @@ def measure_traffic(args, kind):
     if not shutil.which("rocprofv3"):
         return None
     child = [sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
-             "--no-cpu-baseline", "--no-profile", "--no-traffic", "--no-hand", "--no-next",
+             "--no-cpu-baseline", "--no-profile", "--no-traffic", "--no-hand", "--no-next", "--no-tracking",
              "--batch", str(args.batch), "--workload", kind,
              "--sub-batches", str(args.sub_batches), "--streams", args.streams]
     kib, launches = {}, {}
@@ -489,6 +492,8 @@ def main():
         out["hand"] = hand_line(H, args, device)
     if world == 1 and args.workload == "face" and not args.no_next:
         out["face_next"] = next_line(H, args, device)
+    if world == 1 and args.workload == "face" and not args.no_tracking:
+        out["tracking"] = tracking_line(H, args, device, wl)
     out["cpu_baseline"] = cpu
     print(json.dumps(out))
     if world > 1:
@@ -529,6 +534,41 @@ def next_line(H, args, device):
         out["kernels"] = sorted(kernels, key=lambda k: -k["ms"])[:8]
     del w
     return out
+
+
+def tracking_line(H, args, device, wl):
+    """the video loop of LandmarkTracker with its state on the device
+    (DeviceTracker): every frame of the face workload is one stream, seeded with an RoI on its
+    face patch; each step = FaceMesh on the views the previous update wrote + the update kernel,
+    no host round trip.  value = tracked faces (active ROIs) per second."""
+    import torch
+    fs = wl.fs
+    rng = np.random.default_rng(77)
+    rois = []
+    for (y, x) in fs.pos:
+        side = float(rng.uniform(380, 440))
+        rois.append((x + 288.0 + float(rng.uniform(-8, 8)), y + 288.0 + float(rng.uniform(-8, 8)), side, side, 0.0))
+    tr = H.DeviceTracker("facemesh", device, 0.3, 0.5)
+    tr.set_rois(rois, [(fs.w, fs.h)] * len(rois))
+    for _ in range(3):
+        tr.step(wl.flist)
+    tr.synchronize()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.tracking_steps):
+        tr.step(wl.flist)
+    tr.synchronize()
+    elapsed = time.perf_counter() - t0
+    active = sum(1 for st in tr.states() if st["active"])
+    bpf = SURVEY_BYTES["face_landmark"] + 16.0 * 192 * 192
+    fps = active * args.tracking_steps / elapsed
+    return {"metric": "tracked faces/sec, LandmarkTracker video loop with device-resident state "
+                      "(FaceMesh V1 per frame, no detection)",
+            "value": round(fps, 1), "unit": "faces/s", "streams": len(rois), "active_streams": active,
+            "steps": args.tracking_steps, "ms_per_step": round(1e3 * elapsed / args.tracking_steps, 3),
+            "pipeline_roofline": {"model": "SURVEY.md §8d FaceMesh bytes + 192^2 preprocessing per face",
+                                  "bytes_per_face": round(bpf), "achieved_GBs": round(fps * bpf / 1e9, 1),
+                                  "frac": round(fps * bpf / 1e9 / HBM_PEAK_GBS, 4)}}
 
 
 def hand_line(H, args, device):
