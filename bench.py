@@ -95,6 +95,7 @@ def parse():
     ap.add_argument("--no-tracking", action="store_true",
                     help="skip the SURVEY §8f-3 device-tracker line at N = 1")
     ap.add_argument("--tracking-steps", type=int, default=50)
+    ap.add_argument("--no-jpeg", action="store_true", help="skip the SURVEY §8f-2 JPEG-source line at N = 1")
     ap.add_argument("--next-batch", type=int, default=512)
     return ap.parse_args()
 
@@ -190,6 +191,7 @@ def measure_traffic(args, kind):
         return None
     child = [sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
              "--no-cpu-baseline", "--no-profile", "--no-traffic", "--no-hand", "--no-next", "--no-tracking",
+             "--no-jpeg",
              "--batch", str(args.batch), "--workload", kind,
              "--sub-batches", str(args.sub_batches), "--streams", args.streams]
     kib, launches = {}, {}
@@ -494,6 +496,8 @@ def main():
         out["face_next"] = next_line(H, args, device)
     if world == 1 and args.workload == "face" and not args.no_tracking:
         out["tracking"] = tracking_line(H, args, device, wl)
+    if world == 1 and args.workload == "face" and not args.no_jpeg:
+        out["jpeg_source"] = jpeg_line(args, device)
     out["cpu_baseline"] = cpu
     print(json.dumps(out))
     if world > 1:
@@ -569,6 +573,68 @@ def tracking_line(H, args, device, wl):
             "pipeline_roofline": {"model": "SURVEY.md §8d FaceMesh bytes + 192^2 preprocessing per face",
                                   "bytes_per_face": round(bpf), "achieved_GBs": round(fps * bpf / 1e9, 1),
                                   "frac": round(fps * bpf / 1e9 / HBM_PEAK_GBS, 4)}}
+
+
+def jpeg_line(args, device, n_distinct=32, n_decodes=512, threads=16):
+    """1080p JPEG -> RGBA8 frames in HBM, byte-identical to the reference's
+    libjpeg-turbo backend.  `threads` host threads each own a decoder and a HIP stream (entropy
+    decoding is serial per frame; ctypes releases the GIL), the pixel stages run on the GPU.
+    Beside it: libjpeg-turbo itself (Pillow) on one core, the reference's CPU decode."""
+    import io
+    import threading
+    import torch
+    from PIL import Image
+    from zaru_amd import jpeg
+    from zaru_amd._lib import check, lib
+    import ctypes as C
+    rng = np.random.default_rng(55)
+    fs = FrameSet(rng, n_distinct, patch=load_patch())
+    datas = []
+    for i in range(n_distinct):
+        b = io.BytesIO()
+        Image.fromarray(fs.frame(i)[..., :3]).save(b, "JPEG", quality=90)
+        datas.append(b.getvalue())
+    w, h = jpeg.info(datas[0])
+    out = torch.empty((threads, h, w, 4), dtype=torch.uint8, device=f"cuda:{device}")
+    decs, streams = [], []
+    for t in range(threads):
+        decs.append(jpeg.JpegDecoder(device))
+        sp = C.c_void_p()
+        check(lib().zr_stream_create(C.byref(sp)))
+        streams.append(sp.value)
+
+    def work(t, count):
+        for k in range(count):
+            decs[t].decode_into(datas[(t * 7 + k) % n_distinct], out[t].data_ptr(), w * 4, streams[t])
+        check(lib().zr_stream_synchronize(streams[t]))
+
+    def run(total):
+        per = total // threads
+        ths = [threading.Thread(target=work, args=(t, per)) for t in range(threads)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        return per * threads, time.perf_counter() - t0
+
+    run(threads * 2)
+    n, el = run(n_decodes)
+    t0 = time.perf_counter()
+    cpu_n = 0
+    while time.perf_counter() - t0 < 3.0:
+        Image.open(io.BytesIO(datas[cpu_n % n_distinct])).convert("RGBA").load()
+        cpu_n += 1
+    cpu_el = time.perf_counter() - t0
+    for t in range(threads):
+        check(lib().zr_stream_destroy(streams[t]))
+        decs[t].close()
+    mb = sum(len(d) for d in datas) / len(datas) / 1e6
+    return {"metric": "1080p JPEG frames/sec decoded into HBM (RGBA8, byte-identical to libjpeg-turbo)",
+            "value": round(n / el, 1), "unit": "frames/s", "host_threads": threads, "decodes": n,
+            "jpeg_MB_per_frame": round(mb, 3), "quality": 90, "subsampling": "4:2:0",
+            "cpu_libjpeg_turbo_1core": {"value": round(cpu_n / cpu_el, 1), "unit": "frames/s",
+                                        "note": "Pillow's libjpeg-turbo (the reference's libjpeg-turbo backend), one core"}}
 
 
 def hand_line(H, args, device):

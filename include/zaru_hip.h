@@ -155,6 +155,21 @@ int zr_cnn_estimate_device_views_async(zr_session *s, const zr_frame *frames, si
                                        const zr_view_desc *d_views, size_t n_views, float lo,
                                        float hi, float *const *d_outputs, void *hip_stream);
 
+/* ---- JPEG frame source --------------------------------------------------
+ * Replaces decode_jpeg (crates/zaru-image/src/jpeg.rs:107-182) for its libjpeg-turbo backend
+ * (turbojpeg 0.5.3: accurate integer IDCT, fancy upsampling, TJPF_RGBA output): the frame is
+ * decoded straight into an RGBA8 device buffer, byte-identical to libjpeg-turbo.  Entropy
+ * decoding runs on the calling thread; dequantisation, IDCT, upsampling and colour conversion
+ * are enqueued on `hip_stream`.  Baseline 8-bit JPEG, 1 or 3 components, 4:4:4 / 4:2:2 / 4:2:0,
+ * one interleaved scan, restart markers.  A decoder may be reused; calls on one decoder are
+ * serialised (its coefficient staging is reused once the previous upload completed). */
+typedef struct zr_jpeg_decoder zr_jpeg_decoder;
+int zr_jpeg_decoder_create(int device, zr_jpeg_decoder **out);
+void zr_jpeg_decoder_destroy(zr_jpeg_decoder *d);
+int zr_jpeg_info(const uint8_t *jpeg, size_t len, uint32_t *width, uint32_t *height);
+int zr_jpeg_decode_async(zr_jpeg_decoder *d, const uint8_t *jpeg, size_t len, uint8_t *d_rgba,
+                         size_t row_stride, void *hip_stream);
+
 /* Roofline accounting of the compiled plan: algorithmic bytes and FLOPs per image, number
  * of kernel launches per run. */
 int zr_session_stats(const zr_session *s, double *bytes_per_image, double *flops_per_image,

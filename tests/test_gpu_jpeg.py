@@ -1,0 +1,129 @@
+"""the JPEG frame source (zaru_amd.jpeg over zr_jpeg_decode_async) against
+libjpeg-turbo, the library behind the reference's `ZARU_JPEG_BACKEND=libjpeg-turbo` decoder
+(crates/zaru-image/src/jpeg.rs:164-182: turbojpeg 0.5.3, default flags = accurate integer IDCT
+and fancy upsampling, RGBA output with alpha 255).  Pillow in this image links libjpeg-turbo
+and decodes with the same defaults, so it is the reference run here; the bar is byte equality.
+
+The default backend, zune-jpeg 0.3.17 (jpeg.rs:183-205), is not installed anywhere in this
+image, so parity with it is unpinned (it differs from libjpeg-turbo by +-1 in places).
+
+Inputs are synthetic (seeded noise, gradients, a face crop of the reference's own test image),
+encoded by Pillow at several sizes, qualities, chroma subsamplings and restart intervals.
+"""
+import io
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def synthetic(h, w, seed):
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w]
+    img = np.stack([(x * 255 // max(1, w - 1)), (y * 255 // max(1, h - 1)), ((x + y) * 7) % 256], -1)
+    img = (img + rng.integers(-40, 41, size=img.shape)).clip(0, 255).astype(np.uint8)
+    codes = np.load(os.path.join(REPO, "tests", "golden", "sad_linus_mesh.npz"))["codes"][0]
+    ph, pw = min(192, h), min(192, w)
+    img[:ph, :pw] = codes.transpose(1, 2, 0)[:ph, :pw]
+    return img
+
+
+def encode(img, **kw):
+    from PIL import Image
+    b = io.BytesIO()
+    Image.fromarray(img).save(b, "JPEG", **kw)
+    return b.getvalue()
+
+
+def libjpeg_turbo_rgba(data):
+    from PIL import Image
+    return np.asarray(Image.open(io.BytesIO(data)).convert("RGBA"))
+
+
+@pytest.fixture(scope="module")
+def dec():
+    from zaru_amd.jpeg import JpegDecoder
+    d = JpegDecoder(0)
+    yield d
+    d.close()
+
+
+CASES = [
+    # (h, w, quality, subsampling 0=4:4:4 1=4:2:2 2=4:2:0, extra save options)
+    (1080, 1920, 90, 2, {}),
+    (61, 97, 75, 2, {}),
+    (33, 17, 95, 2, {}),
+    (64, 64, 50, 0, {}),
+    (45, 131, 85, 1, {}),
+    (120, 160, 75, 2, {"restart_marker_blocks": 3}),
+    (97, 203, 100, 0, {"restart_marker_rows": 1}),
+]
+
+
+@pytest.mark.parametrize("h,w,q,sub,kw", CASES)
+def test_decode_equals_libjpeg_turbo(dec, h, w, q, sub, kw):
+    data = encode(synthetic(h, w, h * 1000 + w), quality=q, subsampling=sub, **kw)
+    got = dec.decode(data)
+    want = libjpeg_turbo_rgba(data)
+    assert got.shape == want.shape == (h, w, 4)
+    diff = np.abs(got.astype(int) - want.astype(int))
+    assert diff.max() == 0, (h, w, q, sub, int(diff.max()), int((diff > 0).sum()))
+
+
+def test_grayscale(dec):
+    g = synthetic(70, 90, 5)[..., 0]
+    data = encode(g, quality=80)
+    assert np.array_equal(dec.decode(data), libjpeg_turbo_rgba(data))
+
+
+def test_decoder_reuse_across_sizes(dec):
+    """One decoder, shrinking and growing frames: staging reuse never leaks the previous frame."""
+    for i, (h, w) in enumerate([(480, 640), (64, 48), (720, 1280), (480, 640)]):
+        data = encode(synthetic(h, w, 77 + i), quality=85)
+        assert np.array_equal(dec.decode(data), libjpeg_turbo_rgba(data))
+
+
+def test_decoded_frames_feed_the_pipeline(dec):
+    """Frames decoded into HBM by the JPEG source run the config-3 pipeline exactly as frames
+    uploaded from libjpeg-turbo's host decode (same bytes -> same detections and landmarks)."""
+    import zaru_amd.host as H
+    from zaru_amd._lib import DeviceBuffer
+    imgs = [synthetic(360, 640, 900 + i) for i in range(3)]
+    datas = [encode(im, quality=90) for im in imgs]
+    a = DeviceBuffer(3 * 360 * 640 * 4)
+    for i, d in enumerate(datas):
+        dec.decode_into(d, a.ptr + i * 360 * 640 * 4, 640 * 4)
+    from zaru_amd._lib import lib
+    lib().zr_stream_synchronize(None)
+    b = DeviceBuffer.from_array(np.stack([libjpeg_turbo_rgba(d) for d in datas]))
+    forced = [[(320.0, 180.0, 200.0, 200.0, 0.0)] for _ in range(3)]
+    res = []
+    for buf in (a, b):
+        p = H.DetectTrackPipeline("face", 0, 4, 1)
+        p.run([(buf.ptr + i * 360 * 640 * 4, 640, 360, 640 * 4) for i in range(3)], forced)
+        res.append([(r["frame"], r["tracked"], r["landmarks"].tobytes()) for r in (p.roi(i) for i in range(p.num_rois()))])
+    assert res[0] == res[1]
+
+
+@pytest.mark.parametrize("bad", [b"", b"\xff\xd8\xff\xd9", b"not a jpeg at all"])
+def test_malformed_streams_are_errors(dec, bad):
+    from zaru_amd._lib import ZaruError
+    with pytest.raises(ZaruError):
+        dec.decode(bad)
+
+
+def test_truncated_scan_is_decoded_or_rejected(dec):
+    """A stream cut inside the entropy-coded data: the decoder pads with zero bits (libjpeg
+    warns and does the same) -- it must neither crash nor read past the buffer."""
+    data = encode(synthetic(64, 64, 3), quality=90)
+    cut = data[: len(data) * 2 // 3]
+    from zaru_amd._lib import ZaruError
+    try:
+        out = dec.decode(cut)
+    except ZaruError:
+        return
+    assert out.shape == (64, 64, 4)

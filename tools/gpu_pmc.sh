@@ -5,7 +5,7 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=${1:-r02}; shift
 O=gpurun_out/$TAG/pmc && mkdir -p $O &&
-B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-traffic --no-hand --no-next --no-tracking $*"
+B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-traffic --no-hand --no-next --no-tracking --no-jpeg $*"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O -o fetch -- $B > $O/fetch.json 2> $O/fetch.err &&
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O -o write -- $B > $O/write.json 2> $O/write.err &&
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD --kernel-trace --output-format csv -d $O -o sq1 -- $B > $O/sq1.json 2> $O/sq1.err &&

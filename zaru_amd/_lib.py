@@ -53,6 +53,10 @@ SIGNATURES = [
     ("zr_track_seed_async", _I, [_P, _SZ, _P, _P, _P]),
     ("zr_track_update_async", _I, [_P, _SZ, _P, _P, _P, _SZ, _P, _P, _P]),
     ("zr_cnn_estimate_device_views_async", _I, [_P, _P, _SZ, _P, _SZ, _F, _F, _P, _P]),
+    ("zr_jpeg_decoder_create", _I, [C.c_int, _P]),
+    ("zr_jpeg_decoder_destroy", None, [_P]),
+    ("zr_jpeg_info", _I, [_P, _SZ, _P, _P]),
+    ("zr_jpeg_decode_async", _I, [_P, _P, _SZ, _P, _SZ, _P]),
     ("zr_session_stats", _I, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(_SZ)]),
     ("zr_plan_describe", _I, [_P, _SZ, _P, _SZ, _P, _SZ, C.POINTER(_SZ)]),
     ("zr_profile_enable", _I, [_P, _I]),

@@ -1,0 +1,420 @@
+// jpeg.cpp -- the host half of the JPEG frame source: marker parsing and
+// baseline Huffman entropy decoding (ITU T.81 F.2.2) into quantised coefficients, which the
+// device half (kernels/jpeg.hip) turns into RGBA8 frames in HBM.  Entropy decoding is bit-serial
+// within a scan, so it stays on a CPU core, as in every GPU JPEG pipeline; the pixel work
+// (IDCT, upsampling, colour conversion: ~all of libjpeg-turbo's decode time) runs on the GPU.
+// Supported: baseline sequential DCT (SOF0/SOF1), 8-bit samples, 1 or 3 components with luma
+// sampling 1x1 / 2x1 / 2x2 over 1x1 chroma, one interleaved scan, restart intervals.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../../include/zaru_hip.h"
+#include "zr_jpeg.h"
+
+namespace zr_internal {
+int set_error(int code, const std::string &msg);
+}
+
+namespace {
+
+constexpr uint8_t ZIGZAG[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                                12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                                35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                                58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+struct Huff {
+    bool present = false;
+    // canonical decoding (T.81 F.2.2.3): per code length the largest code and symbol offset
+    int32_t maxcode[18];
+    int32_t valoff[17];
+    uint8_t vals[256];
+    // 9-bit lookahead: (length << 8) | symbol, 0 = longer code
+    uint16_t look[512];
+};
+
+struct Comp {
+    int id, h, v, tq, td, ta;
+};
+
+struct Header {
+    int W = 0, H = 0, ncomp = 0;
+    Comp comp[3];
+    uint16_t q[4][64];  // natural order
+    bool qpresent[4] = {false, false, false, false};
+    Huff dc[4], ac[4];
+    int restart = 0;
+    size_t scan_begin = 0;  // entropy-coded data
+};
+
+struct JpegError {
+    int code;
+    std::string msg;
+};
+
+[[noreturn]] void fail(const std::string &m) { throw JpegError{ZR_ERR_INVALID_ARGUMENT, "jpeg: " + m}; }
+
+void build_huff(Huff &h, const uint8_t *counts, const uint8_t *vals, int nvals) {
+    h.present = true;
+    std::memcpy(h.vals, vals, nvals);
+    int code = 0, k = 0;
+    std::memset(h.look, 0, sizeof h.look);
+    for (int len = 1; len <= 16; len++) {
+        h.valoff[len] = k - code;
+        for (int i = 0; i < counts[len - 1]; i++) {
+            if (len <= 9) {  // fill every 9-bit lookahead slot this code prefixes
+                const int shift = 9 - len;
+                for (int f = 0; f < (1 << shift); f++) h.look[(code << shift) | f] = (uint16_t)((len << 8) | vals[k]);
+            }
+            code++;
+            k++;
+        }
+        h.maxcode[len] = counts[len - 1] ? code - 1 : -1;
+        if (code > (1 << len)) fail("bad Huffman table");
+        code <<= 1;
+    }
+    h.maxcode[17] = 0x7fffffff;
+}
+
+void parse(const uint8_t *d, size_t n, Header &hd) {
+    if (n < 4 || d[0] != 0xFF || d[1] != 0xD8) fail("missing SOI");
+    size_t p = 2;
+    bool sof = false;
+    while (p + 4 <= n) {
+        if (d[p] != 0xFF) fail("marker expected");
+        const uint8_t m = d[p + 1];
+        if (m == 0xFF) {
+            p++;
+            continue;
+        }
+        p += 2;
+        if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
+        if (m == 0xD9) fail("no scan");
+        const size_t len = ((size_t)d[p] << 8) | d[p + 1];
+        if (len < 2 || p + len > n) fail("truncated segment");
+        const uint8_t *s = d + p + 2;
+        const size_t sl = len - 2;
+        if (m == 0xDB) {  // DQT
+            size_t i = 0;
+            while (i < sl) {
+                const int pq = s[i] >> 4, tq = s[i] & 15;
+                if (tq > 3 || pq > 1 || i + 1 + 64 * (pq + 1) > sl) fail("bad DQT");
+                for (int k = 0; k < 64; k++)
+                    hd.q[tq][ZIGZAG[k]] = pq ? (uint16_t)((s[i + 1 + 2 * k] << 8) | s[i + 2 + 2 * k]) : s[i + 1 + k];
+                hd.qpresent[tq] = true;
+                i += 1 + 64 * (pq + 1);
+            }
+        } else if (m == 0xC4) {  // DHT
+            size_t i = 0;
+            while (i < sl) {
+                if (i + 17 > sl) fail("bad DHT");
+                const int tc = s[i] >> 4, th = s[i] & 15;
+                int tot = 0;
+                for (int k = 0; k < 16; k++) tot += s[i + 1 + k];
+                if (tc > 1 || th > 3 || tot > 256 || i + 17 + tot > sl) fail("bad DHT");
+                build_huff(tc ? hd.ac[th] : hd.dc[th], s + i + 1, s + i + 17, tot);
+                i += 17 + tot;
+            }
+        } else if (m == 0xC0 || m == 0xC1) {  // SOF0 / SOF1 (baseline / extended Huffman)
+            if (sl < 6 || s[0] != 8) fail("only 8-bit baseline frames are supported");
+            hd.H = (s[1] << 8) | s[2];
+            hd.W = (s[3] << 8) | s[4];
+            hd.ncomp = s[5];
+            if (hd.W <= 0 || hd.H <= 0 || hd.W > 16384 || hd.H > 16384) fail("bad frame size");
+            if ((hd.ncomp != 1 && hd.ncomp != 3) || sl < 6 + 3 * (size_t)hd.ncomp) fail("1 or 3 components only");
+            for (int c = 0; c < hd.ncomp; c++) {
+                hd.comp[c].id = s[6 + 3 * c];
+                hd.comp[c].h = s[7 + 3 * c] >> 4;
+                hd.comp[c].v = s[7 + 3 * c] & 15;
+                hd.comp[c].tq = s[8 + 3 * c];
+                if (hd.comp[c].tq > 3) fail("bad quant table selector");
+            }
+            if (hd.ncomp == 1) hd.comp[0].h = hd.comp[0].v = 1;
+            sof = true;
+        } else if ((m >= 0xC2 && m <= 0xCF) && m != 0xC4 && m != 0xC8 && m != 0xCC) {
+            fail("progressive / lossless / arithmetic JPEG is not supported");
+        } else if (m == 0xDD) {  // DRI
+            if (sl < 2) fail("bad DRI");
+            hd.restart = (s[0] << 8) | s[1];
+        } else if (m == 0xDA) {  // SOS
+            if (!sof) fail("SOS before SOF");
+            const int ns = s[0];
+            if (ns != hd.ncomp || sl < 1 + 2 * (size_t)ns + 3) fail("only one interleaved scan of all components");
+            for (int k = 0; k < ns; k++) {
+                const int id = s[1 + 2 * k], t = s[2 + 2 * k];
+                int c = -1;
+                for (int j = 0; j < hd.ncomp; j++)
+                    if (hd.comp[j].id == id) c = j;
+                if (c != k) fail("scan component order");
+                hd.comp[c].td = t >> 4;
+                hd.comp[c].ta = t & 15;
+                if (hd.comp[c].td > 3 || hd.comp[c].ta > 3 || !hd.dc[hd.comp[c].td].present ||
+                    !hd.ac[hd.comp[c].ta].present || !hd.qpresent[hd.comp[c].tq])
+                    fail("missing tables");
+            }
+            hd.scan_begin = p + len;
+            return;
+        }
+        p += len;
+    }
+    fail("truncated stream");
+}
+
+struct Bits {
+    const uint8_t *d;
+    size_t n, p;
+    uint64_t acc = 0;
+    int cnt = 0;
+    bool marker = false;  // a marker was reached: feed zeros (T.81 F.2.2.5 leaves this to us)
+    void fill() {
+        while (cnt <= 56) {
+            uint32_t b = 0;
+            if (!marker && p < n) {
+                b = d[p];
+                if (b == 0xFF) {
+                    const uint8_t nx = p + 1 < n ? d[p + 1] : 0xD9;
+                    if (nx == 0x00) {
+                        p += 2;
+                    } else {
+                        marker = true;
+                        b = 0;
+                    }
+                } else {
+                    p++;
+                }
+            }
+            acc |= (uint64_t)b << (56 - cnt);
+            cnt += 8;
+        }
+    }
+    uint32_t peek(int k) {
+        if (cnt < k) fill();
+        return (uint32_t)(acc >> (64 - k));
+    }
+    void skip(int k) {
+        acc <<= k;
+        cnt -= k;
+    }
+    int get(int k) {
+        if (k == 0) return 0;
+        const uint32_t v = peek(k);
+        skip(k);
+        return (int)v;
+    }
+    void restart() {  // drop the padding bits, consume the RSTn marker (T.81 F.2.2.5)
+        acc = 0;
+        cnt = 0;
+        marker = false;
+        while (p + 1 < n && !(d[p] == 0xFF && d[p + 1] >= 0xD0 && d[p + 1] <= 0xD7)) p++;
+        if (p + 1 < n) p += 2;
+    }
+};
+
+inline int decode(Bits &b, const Huff &h) {
+    const uint32_t l = b.peek(9);
+    const uint16_t e = h.look[l];
+    if (e) {
+        b.skip(e >> 8);
+        return e & 0xFF;
+    }
+    uint32_t code = b.peek(16);
+    for (int len = 10; len <= 16; len++) {
+        const int32_t c = (int32_t)(code >> (16 - len));
+        if (c <= h.maxcode[len]) {
+            b.skip(len);
+            return h.vals[c + h.valoff[len]];
+        }
+    }
+    fail("bad Huffman code");
+}
+
+inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
+
+}  // namespace
+
+struct zr_jpeg_decoder {
+    int device = 0;
+    std::mutex mu;
+    int16_t *h_coef = nullptr, *d_coef = nullptr;
+    size_t coef_cap = 0;  // blocks
+    uint8_t *d_planes = nullptr;
+    size_t planes_cap = 0;
+    hipEvent_t staged = nullptr;  // the last H2D copy out of h_coef has completed
+};
+
+namespace {
+int err(int code, const std::string &m) { return zr_internal::set_error(code, m); }
+}  // namespace
+
+extern "C" {
+
+int zr_jpeg_decoder_create(int device, zr_jpeg_decoder **out) {
+    try {
+        if (!out) return err(ZR_ERR_INVALID_ARGUMENT, "null out");
+        *out = nullptr;
+        if (hipSetDevice(device) != hipSuccess) return err(ZR_ERR_DEVICE, "hipSetDevice failed");
+        auto *d = new zr_jpeg_decoder();
+        d->device = device;
+        if (hipEventCreateWithFlags(&d->staged, hipEventDisableTiming) != hipSuccess) {
+            delete d;
+            return err(ZR_ERR_DEVICE, "hipEventCreate failed");
+        }
+        *out = d;
+        return ZR_OK;
+    } catch (...) {
+        return err(ZR_ERR_INTERNAL, "jpeg decoder creation failed");
+    }
+}
+
+void zr_jpeg_decoder_destroy(zr_jpeg_decoder *d) {
+    if (!d) return;
+    (void)hipEventSynchronize(d->staged);
+    (void)hipEventDestroy(d->staged);
+    (void)hipHostFree(d->h_coef);
+    (void)hipFree(d->d_coef);
+    (void)hipFree(d->d_planes);
+    delete d;
+}
+
+int zr_jpeg_info(const uint8_t *jpeg, size_t len, uint32_t *width, uint32_t *height) {
+    try {
+        if (!jpeg || !width || !height) return err(ZR_ERR_INVALID_ARGUMENT, "null argument");
+        Header hd;
+        parse(jpeg, len, hd);
+        *width = (uint32_t)hd.W;
+        *height = (uint32_t)hd.H;
+        return ZR_OK;
+    } catch (const JpegError &e) {
+        return err(e.code, e.msg);
+    } catch (...) {
+        return err(ZR_ERR_INTERNAL, "jpeg: internal error");
+    }
+}
+
+int zr_jpeg_decode_async(zr_jpeg_decoder *dec, const uint8_t *jpeg, size_t len, uint8_t *d_rgba,
+                         size_t row_stride, void *hip_stream) {
+    try {
+        if (!dec || !jpeg || !d_rgba) return err(ZR_ERR_INVALID_ARGUMENT, "null argument");
+        std::lock_guard<std::mutex> g(dec->mu);
+        Header hd;
+        parse(jpeg, len, hd);
+        if (row_stride < (size_t)hd.W * 4) return err(ZR_ERR_INVALID_ARGUMENT, "row_stride < 4*width");
+        int hmax = 1, vmax = 1;
+        for (int c = 0; c < hd.ncomp; c++) {
+            hmax = std::max(hmax, hd.comp[c].h);
+            vmax = std::max(vmax, hd.comp[c].v);
+        }
+        if (hd.ncomp == 3) {
+            const bool luma_ok = (hd.comp[0].h == 1 && hd.comp[0].v == 1) || (hd.comp[0].h == 2 && hd.comp[0].v == 1) ||
+                                 (hd.comp[0].h == 2 && hd.comp[0].v == 2);
+            if (!luma_ok || hd.comp[1].h != 1 || hd.comp[1].v != 1 || hd.comp[2].h != 1 || hd.comp[2].v != 1)
+                return err(ZR_ERR_INVALID_ARGUMENT, "jpeg: sampling must be 4:4:4, 4:2:2 or 4:2:0");
+        }
+        const int mcux = (hd.W + 8 * hmax - 1) / (8 * hmax), mcuy = (hd.H + 8 * vmax - 1) / (8 * vmax);
+        zr::JpegParams P{};
+        P.ncomp = hd.ncomp;
+        int64_t blocks = 0, pbytes = 0;
+        for (int c = 0; c < hd.ncomp; c++) {
+            P.bw[c] = mcux * hd.comp[c].h;
+            P.bh[c] = mcuy * hd.comp[c].v;
+            P.coef_off[c] = blocks;
+            P.plane_off[c] = pbytes;
+            P.qsel[c] = hd.comp[c].tq;
+            blocks += (int64_t)P.bw[c] * P.bh[c];
+            pbytes += (int64_t)P.bw[c] * P.bh[c] * 64;
+        }
+        std::memcpy(P.q, hd.q, sizeof P.q);
+        P.total_blocks = (int)blocks;
+        // stage the coefficients: the previous decode's copy out of the staging must be done
+        if (hipSetDevice(dec->device) != hipSuccess) return err(ZR_ERR_DEVICE, "hipSetDevice failed");
+        if (hipEventSynchronize(dec->staged) != hipSuccess) return err(ZR_ERR_DEVICE, "event sync failed");
+        if ((size_t)blocks > dec->coef_cap) {
+            (void)hipHostFree(dec->h_coef);
+            (void)hipFree(dec->d_coef);
+            dec->h_coef = nullptr;
+            dec->d_coef = nullptr;
+            dec->coef_cap = 0;
+            const size_t cap = (size_t)blocks + (size_t)blocks / 4;
+            if (hipHostMalloc((void **)&dec->h_coef, cap * 128) != hipSuccess ||
+                hipMalloc((void **)&dec->d_coef, cap * 128) != hipSuccess)
+                return err(ZR_ERR_DEVICE, "jpeg: out of memory");
+            dec->coef_cap = cap;
+        }
+        if ((size_t)pbytes > dec->planes_cap) {
+            (void)hipFree(dec->d_planes);
+            dec->d_planes = nullptr;
+            dec->planes_cap = 0;
+            const size_t cap = (size_t)pbytes + (size_t)pbytes / 4;
+            if (hipMalloc((void **)&dec->d_planes, cap) != hipSuccess) return err(ZR_ERR_DEVICE, "jpeg: out of memory");
+            dec->planes_cap = cap;
+        }
+        // entropy decoding (T.81 F.2.2): MCU by MCU, components in scan order, h x v blocks each
+        int16_t *coef = dec->h_coef;
+        std::memset(coef, 0, (size_t)blocks * 128);
+        Bits bits{jpeg, len, hd.scan_begin};
+        int pred[3] = {0, 0, 0};
+        const int nmcu = mcux * mcuy;
+        for (int m = 0; m < nmcu; m++) {
+            if (hd.restart && m > 0 && m % hd.restart == 0) {
+                bits.restart();
+                pred[0] = pred[1] = pred[2] = 0;
+            }
+            const int my = m / mcux, mx = m - my * mcux;
+            for (int c = 0; c < hd.ncomp; c++) {
+                const Comp &cp = hd.comp[c];
+                const Huff &dc = hd.dc[cp.td], &ac = hd.ac[cp.ta];
+                for (int v = 0; v < cp.v; v++)
+                    for (int h = 0; h < cp.h; h++) {
+                        const int by = my * cp.v + v, bx = mx * cp.h + h;
+                        int16_t *blk = coef + (P.coef_off[c] + (int64_t)by * P.bw[c] + bx) * 64;
+                        const int s = decode(bits, dc);
+                        if (s > 11) fail("bad DC category");
+                        pred[c] += s ? extend(bits.get(s), s) : 0;
+                        blk[0] = (int16_t)pred[c];
+                        for (int k = 1; k < 64;) {
+                            const int rs = decode(bits, ac);
+                            const int r = rs >> 4, sz = rs & 15;
+                            if (sz) {
+                                k += r;
+                                if (k > 63) fail("AC index out of range");
+                                blk[ZIGZAG[k]] = (int16_t)extend(bits.get(sz), sz);
+                                k++;
+                            } else {
+                                if (r != 15) break;
+                                k += 16;
+                            }
+                        }
+                    }
+            }
+        }
+        hipStream_t st = (hipStream_t)hip_stream;
+        if (hipMemcpyAsync(dec->d_coef, coef, (size_t)blocks * 128, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipEventRecord(dec->staged, st) != hipSuccess)
+            return err(ZR_ERR_DEVICE, "jpeg: coefficient upload failed");
+        P.coef = dec->d_coef;
+        P.planes = dec->d_planes;
+        P.W = hd.W;
+        P.H = hd.H;
+        P.hs = hd.ncomp == 3 ? hd.comp[0].h : 1;
+        P.vs = hd.ncomp == 3 ? hd.comp[0].v : 1;
+        P.cw = hd.ncomp == 3 ? (hd.W + P.hs - 1) / P.hs : 0;  // downsampled_width (jdinput.c)
+        P.ch = hd.ncomp == 3 ? (hd.H + P.vs - 1) / P.vs : 0;
+        P.out = d_rgba;
+        P.out_stride = (int64_t)row_stride;
+        zr::launch_jpeg(P, st);
+        if (hipGetLastError() != hipSuccess) return err(ZR_ERR_DEVICE, "jpeg: kernel launch failed");
+        return ZR_OK;
+    } catch (const JpegError &e) {
+        return err(e.code, e.msg);
+    } catch (const std::bad_alloc &) {
+        return err(ZR_ERR_INTERNAL, "jpeg: out of host memory");
+    } catch (...) {
+        return err(ZR_ERR_INTERNAL, "jpeg: internal error");
+    }
+}
+
+}  // extern "C"

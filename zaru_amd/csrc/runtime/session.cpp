@@ -30,6 +30,16 @@ int set_err(int code, const std::string &msg) noexcept {
     return code;
 }
 
+}  // namespace
+
+// the thread-local error of the C ABI, for entry points defined in other translation units
+// (runtime/jpeg.cpp)
+namespace zr_internal {
+int set_error(int code, const std::string &msg) { return set_err(code, msg); }
+}  // namespace zr_internal
+
+namespace {
+
 // Every extern "C" entry point runs its body through this: no C++ exception crosses the C
 // boundary (zaru_hip.h; a throw into the Rust caller's FFI frame is undefined behaviour).
 // std::bad_alloc (host allocations: pools, staging vectors, strings) maps to ZR_ERR_DEVICE's
