@@ -381,11 +381,13 @@ def main():
 
     import torch
     import torch.distributed as dist
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    device = local if world > 1 else 0
+    # ZARU_BENCH_SHARE_GPU=1: a dry run of the N > 1 path on a one-GPU box -- every rank on
+    # cuda:0 and the record gather over gloo (RCCL refuses two ranks on one device)
+    share = world > 1 and os.environ.get("ZARU_BENCH_SHARE_GPU") == "1"
+    device = 0 if (share or world == 1) else local
     torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("gloo" if share else "nccl")
 
     import zaru_amd.host as H
     from zaru_amd import shard
@@ -396,8 +398,8 @@ def main():
     for k in kinds:  # config 5: the hand pipeline runs on the face pipeline's frames
         wls.append(Workload(H, k, device, args.batch, rank, threads, args.sub_batches,
                             args.streams == "multi", shared=wls[0] if wls else None))
-    gather = (shard.RecordGather(args.batch * len(wls), shard.record_width(), f"cuda:{device}")
-              if world > 1 else None)
+    gather = (shard.RecordGather(args.batch * len(wls), shard.record_width(),
+                                 "cpu" if share else f"cuda:{device}") if world > 1 else None)
     pool = None
     if len(wls) > 1:
         from concurrent.futures import ThreadPoolExecutor
@@ -416,10 +418,11 @@ def main():
 
     counts = np.array([[t["tracked"], t["rois"], t["frames"], t["detections"]] for t in times], np.float64)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
+        red_dev = "cpu" if share else f"cuda:{device}"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        c = torch.from_numpy(counts).to(f"cuda:{device}")
+        c = torch.from_numpy(counts).to(red_dev)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         counts = c.cpu().numpy()
     if rank != 0:
