@@ -169,6 +169,15 @@ void zr_jpeg_decoder_destroy(zr_jpeg_decoder *d);
 int zr_jpeg_info(const uint8_t *jpeg, size_t len, uint32_t *width, uint32_t *height);
 int zr_jpeg_decode_async(zr_jpeg_decoder *d, const uint8_t *jpeg, size_t len, uint8_t *d_rgba,
                          size_t row_stride, void *hip_stream);
+/* Host-only half (no GPU): the frame's block layout and, when `coef` is given, its quantised
+ * coefficients ([component][by][bx][64], natural order; cap_blocks >= layout->total_blocks). */
+typedef struct {
+    uint32_t width, height, ncomp, h_samp, v_samp, total_blocks;
+    uint32_t bw[3], bh[3], qsel[3];
+    uint16_t quant[4][64]; /* natural order */
+} zr_jpeg_layout;
+int zr_jpeg_coefficients(const uint8_t *jpeg, size_t len, int16_t *coef, size_t cap_blocks,
+                         zr_jpeg_layout *layout);
 
 /* Roofline accounting of the compiled plan: algorithmic bytes and FLOPs per image, number
  * of kernel launches per run. */

@@ -139,6 +139,8 @@ def _lib():
     L.zo_net_run_f64out.argtypes = [P, P, P]
     L.zo_net_error.restype = C.c_char_p
     L.zo_net_tensor.restype = sz
+    L.zo_jpeg_pixels.restype = C.c_int
+    L.zo_jpeg_pixels.argtypes = [P, u32, u32, u32, u32, u32, P, P, P, P, P]
     L.zo_net_tensor.argtypes = [P, C.c_char_p, P, sz, P, P]
     _LIB = L
     return L
@@ -344,3 +346,20 @@ class Net:
         out = np.empty(n, np.float64)
         _lib().zo_net_tensor(self._h, name.encode(), _ptr(out), n, None, None)
         return out.reshape(tuple(int(v) for v in shape[:rank.value]))
+
+
+# ---------------------------------------------------------------- JPEG (libjpeg-turbo pixels)
+def jpeg_pixels(coef: np.ndarray, layout: dict) -> np.ndarray:
+    """libjpeg-turbo's islow IDCT + fancy upsampling + YCbCr->RGBA (oracle/jpeg.c) over the
+    quantised coefficients of one frame (zaru_amd.jpeg.coefficients)."""
+    coef = np.ascontiguousarray(coef, np.int16)
+    bw = np.ascontiguousarray(layout["bw"], np.uint32)
+    bh = np.ascontiguousarray(layout["bh"], np.uint32)
+    qs = np.ascontiguousarray(layout["qsel"], np.uint32)
+    q = np.ascontiguousarray(layout["quant"], np.uint16)
+    out = np.empty((layout["height"], layout["width"], 4), np.uint8)
+    if _lib().zo_jpeg_pixels(_ptr(coef), layout["width"], layout["height"], layout["ncomp"],
+                             layout["h_samp"], layout["v_samp"], _ptr(bw), _ptr(bh), _ptr(qs),
+                             _ptr(q), _ptr(out)):
+        raise MemoryError("zo_jpeg_pixels")
+    return out

@@ -97,6 +97,10 @@ size_t zo_net_output_shape(const zo_net *n, size_t idx, int64_t *shape);
 /* input: NCHW 1x3xHxW float; outputs: float arrays sized per output shape. 0 on success */
 int zo_net_run(zo_net *n, const float *input, float *const *outputs);
 const char *zo_net_error(void);
+/* libjpeg-turbo's pixel stages (jpeg.c): quantised coefficients -> RGBA8 */
+int zo_jpeg_pixels(const int16_t *coef, uint32_t width, uint32_t height, uint32_t ncomp,
+                   uint32_t h_samp, uint32_t v_samp, const uint32_t *bw, const uint32_t *bh,
+                   const uint32_t *qsel, const uint16_t *quant, uint8_t *rgba);
 size_t zo_net_tensor(const zo_net *n, const char *name, double *out, size_t cap, int64_t *shape,
                      size_t *rank);
 

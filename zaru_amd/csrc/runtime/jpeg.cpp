@@ -35,6 +35,9 @@ struct Huff {
     uint8_t vals[256];
     // 9-bit lookahead: (length << 8) | symbol, 0 = longer code
     uint16_t look[512];
+    // AC only: code + magnitude bits within the 9-bit lookahead decoded in one step:
+    // (value << 8) | (run << 4) | total bits, 0 = take the slow path
+    int16_t fast_ac[512];
 };
 
 struct Comp {
@@ -78,6 +81,16 @@ void build_huff(Huff &h, const uint8_t *counts, const uint8_t *vals, int nvals) 
         code <<= 1;
     }
     h.maxcode[17] = 0x7fffffff;
+    for (int i = 0; i < 512; i++) {  // stb_image-style fast AC entries (values fit int8 here)
+        h.fast_ac[i] = 0;
+        const uint16_t e = h.look[i];
+        if (!e) continue;
+        const int len = e >> 8, rs = e & 0xFF, run = rs >> 4, size = rs & 15;
+        if (size == 0 || len + size > 9 || size > 7) continue;
+        const int bits = (i >> (9 - len - size)) & ((1 << size) - 1);
+        const int v = bits < (1 << (size - 1)) ? bits - (1 << size) + 1 : bits;
+        h.fast_ac[i] = (int16_t)((v * 256) | (run << 4) | (len + size));
+    }
 }
 
 void parse(const uint8_t *d, size_t n, Header &hd) {
@@ -248,6 +261,96 @@ struct zr_jpeg_decoder {
 
 namespace {
 int err(int code, const std::string &m) { return zr_internal::set_error(code, m); }
+
+
+// Frame layout + entropy decoding shared by the device decode and the host coefficient dump.
+void layout_of(const Header &hd, zr::JpegParams &P) {
+    int hmax = 1, vmax = 1;
+    for (int c = 0; c < hd.ncomp; c++) {
+        hmax = std::max(hmax, hd.comp[c].h);
+        vmax = std::max(vmax, hd.comp[c].v);
+    }
+    if (hd.ncomp == 3) {
+        const bool luma_ok = (hd.comp[0].h == 1 && hd.comp[0].v == 1) || (hd.comp[0].h == 2 && hd.comp[0].v == 1) ||
+                             (hd.comp[0].h == 2 && hd.comp[0].v == 2);
+        if (!luma_ok || hd.comp[1].h != 1 || hd.comp[1].v != 1 || hd.comp[2].h != 1 || hd.comp[2].v != 1)
+            fail("sampling must be 4:4:4, 4:2:2 or 4:2:0");
+    }
+    const int mcux = (hd.W + 8 * hmax - 1) / (8 * hmax), mcuy = (hd.H + 8 * vmax - 1) / (8 * vmax);
+    P = zr::JpegParams{};
+    P.ncomp = hd.ncomp;
+    int64_t blocks = 0, pbytes = 0;
+    for (int c = 0; c < hd.ncomp; c++) {
+        P.bw[c] = mcux * hd.comp[c].h;
+        P.bh[c] = mcuy * hd.comp[c].v;
+        P.coef_off[c] = blocks;
+        P.plane_off[c] = pbytes;
+        P.qsel[c] = hd.comp[c].tq;
+        blocks += (int64_t)P.bw[c] * P.bh[c];
+        pbytes += (int64_t)P.bw[c] * P.bh[c] * 64;
+    }
+    std::memcpy(P.q, hd.q, sizeof P.q);
+    P.total_blocks = (int)blocks;
+    P.W = hd.W;
+    P.H = hd.H;
+    P.hs = hd.ncomp == 3 ? hd.comp[0].h : 1;
+    P.vs = hd.ncomp == 3 ? hd.comp[0].v : 1;
+    P.cw = hd.ncomp == 3 ? (hd.W + P.hs - 1) / P.hs : 0;  // downsampled_width (jdinput.c)
+    P.ch = hd.ncomp == 3 ? (hd.H + P.vs - 1) / P.vs : 0;
+}
+
+// T.81 F.2.2: MCU by MCU, components in scan order, h x v blocks each; every block written
+// whole (zeroed, then its nonzero coefficients), so `coef` needs no clearing beforehand.
+void entropy_decode(const Header &hd, const zr::JpegParams &P, const uint8_t *jpeg, size_t len, int16_t *coef) {
+    Bits bits{jpeg, len, hd.scan_begin};
+    int pred[3] = {0, 0, 0};
+    const int mcux = P.bw[0] / hd.comp[0].h, mcuy = P.bh[0] / hd.comp[0].v;
+    const int nmcu = mcux * mcuy;
+    for (int m = 0; m < nmcu; m++) {
+        if (hd.restart && m > 0 && m % hd.restart == 0) {
+            bits.restart();
+            pred[0] = pred[1] = pred[2] = 0;
+        }
+        const int my = m / mcux, mx = m - my * mcux;
+        for (int c = 0; c < hd.ncomp; c++) {
+            const Comp &cp = hd.comp[c];
+            const Huff &dc = hd.dc[cp.td], &ac = hd.ac[cp.ta];
+            for (int v = 0; v < cp.v; v++)
+                for (int h = 0; h < cp.h; h++) {
+                    const int by = my * cp.v + v, bx = mx * cp.h + h;
+                    int16_t *blk = coef + (P.coef_off[c] + (int64_t)by * P.bw[c] + bx) * 64;
+                    std::memset(blk, 0, 128);
+                    const int s = decode(bits, dc);
+                    if (s > 11) fail("bad DC category");
+                    pred[c] += s ? extend(bits.get(s), s) : 0;
+                    blk[0] = (int16_t)pred[c];
+                    for (int k = 1; k < 64;) {
+                        const int fa = ac.fast_ac[bits.peek(9)];
+                        if (fa) {  // run, size and magnitude in one lookup
+                            k += (fa >> 4) & 15;
+                            bits.skip(fa & 15);
+                            if (k > 63) fail("AC index out of range");
+                            blk[ZIGZAG[k]] = (int16_t)(fa >> 8);
+                            k++;
+                            continue;
+                        }
+                        const int rs = decode(bits, ac);
+                        const int r = rs >> 4, sz = rs & 15;
+                        if (sz) {
+                            k += r;
+                            if (k > 63) fail("AC index out of range");
+                            blk[ZIGZAG[k]] = (int16_t)extend(bits.get(sz), sz);
+                            k++;
+                        } else {
+                            if (r != 15) break;
+                            k += 16;
+                        }
+                    }
+                }
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -295,6 +398,38 @@ int zr_jpeg_info(const uint8_t *jpeg, size_t len, uint32_t *width, uint32_t *hei
     }
 }
 
+int zr_jpeg_coefficients(const uint8_t *jpeg, size_t len, int16_t *coef, size_t cap_blocks,
+                         zr_jpeg_layout *layout) {
+    try {
+        if (!jpeg || !layout) return err(ZR_ERR_INVALID_ARGUMENT, "null argument");
+        Header hd;
+        parse(jpeg, len, hd);
+        zr::JpegParams P;
+        layout_of(hd, P);
+        std::memset(layout, 0, sizeof *layout);
+        layout->width = (uint32_t)hd.W;
+        layout->height = (uint32_t)hd.H;
+        layout->ncomp = (uint32_t)hd.ncomp;
+        layout->h_samp = (uint32_t)P.hs;
+        layout->v_samp = (uint32_t)P.vs;
+        layout->total_blocks = (uint32_t)P.total_blocks;
+        for (int c = 0; c < hd.ncomp; c++) {
+            layout->bw[c] = (uint32_t)P.bw[c];
+            layout->bh[c] = (uint32_t)P.bh[c];
+            layout->qsel[c] = (uint32_t)P.qsel[c];
+        }
+        std::memcpy(layout->quant, P.q, sizeof layout->quant);
+        if (!coef) return ZR_OK;  // layout only
+        if (cap_blocks < (size_t)P.total_blocks) return err(ZR_ERR_INVALID_ARGUMENT, "coefficient buffer too small");
+        entropy_decode(hd, P, jpeg, len, coef);
+        return ZR_OK;
+    } catch (const JpegError &e) {
+        return err(e.code, e.msg);
+    } catch (...) {
+        return err(ZR_ERR_INTERNAL, "jpeg: internal error");
+    }
+}
+
 int zr_jpeg_decode_async(zr_jpeg_decoder *dec, const uint8_t *jpeg, size_t len, uint8_t *d_rgba,
                          size_t row_stride, void *hip_stream) {
     try {
@@ -303,32 +438,10 @@ int zr_jpeg_decode_async(zr_jpeg_decoder *dec, const uint8_t *jpeg, size_t len, 
         Header hd;
         parse(jpeg, len, hd);
         if (row_stride < (size_t)hd.W * 4) return err(ZR_ERR_INVALID_ARGUMENT, "row_stride < 4*width");
-        int hmax = 1, vmax = 1;
-        for (int c = 0; c < hd.ncomp; c++) {
-            hmax = std::max(hmax, hd.comp[c].h);
-            vmax = std::max(vmax, hd.comp[c].v);
-        }
-        if (hd.ncomp == 3) {
-            const bool luma_ok = (hd.comp[0].h == 1 && hd.comp[0].v == 1) || (hd.comp[0].h == 2 && hd.comp[0].v == 1) ||
-                                 (hd.comp[0].h == 2 && hd.comp[0].v == 2);
-            if (!luma_ok || hd.comp[1].h != 1 || hd.comp[1].v != 1 || hd.comp[2].h != 1 || hd.comp[2].v != 1)
-                return err(ZR_ERR_INVALID_ARGUMENT, "jpeg: sampling must be 4:4:4, 4:2:2 or 4:2:0");
-        }
-        const int mcux = (hd.W + 8 * hmax - 1) / (8 * hmax), mcuy = (hd.H + 8 * vmax - 1) / (8 * vmax);
-        zr::JpegParams P{};
-        P.ncomp = hd.ncomp;
-        int64_t blocks = 0, pbytes = 0;
-        for (int c = 0; c < hd.ncomp; c++) {
-            P.bw[c] = mcux * hd.comp[c].h;
-            P.bh[c] = mcuy * hd.comp[c].v;
-            P.coef_off[c] = blocks;
-            P.plane_off[c] = pbytes;
-            P.qsel[c] = hd.comp[c].tq;
-            blocks += (int64_t)P.bw[c] * P.bh[c];
-            pbytes += (int64_t)P.bw[c] * P.bh[c] * 64;
-        }
-        std::memcpy(P.q, hd.q, sizeof P.q);
-        P.total_blocks = (int)blocks;
+        zr::JpegParams P;
+        layout_of(hd, P);
+        const int64_t blocks = P.total_blocks;
+        const int64_t pbytes = blocks * 64;
         // stage the coefficients: the previous decode's copy out of the staging must be done
         if (hipSetDevice(dec->device) != hipSuccess) return err(ZR_ERR_DEVICE, "hipSetDevice failed");
         if (hipEventSynchronize(dec->staged) != hipSuccess) return err(ZR_ERR_DEVICE, "event sync failed");
@@ -352,57 +465,13 @@ int zr_jpeg_decode_async(zr_jpeg_decoder *dec, const uint8_t *jpeg, size_t len, 
             if (hipMalloc((void **)&dec->d_planes, cap) != hipSuccess) return err(ZR_ERR_DEVICE, "jpeg: out of memory");
             dec->planes_cap = cap;
         }
-        // entropy decoding (T.81 F.2.2): MCU by MCU, components in scan order, h x v blocks each
-        int16_t *coef = dec->h_coef;
-        std::memset(coef, 0, (size_t)blocks * 128);
-        Bits bits{jpeg, len, hd.scan_begin};
-        int pred[3] = {0, 0, 0};
-        const int nmcu = mcux * mcuy;
-        for (int m = 0; m < nmcu; m++) {
-            if (hd.restart && m > 0 && m % hd.restart == 0) {
-                bits.restart();
-                pred[0] = pred[1] = pred[2] = 0;
-            }
-            const int my = m / mcux, mx = m - my * mcux;
-            for (int c = 0; c < hd.ncomp; c++) {
-                const Comp &cp = hd.comp[c];
-                const Huff &dc = hd.dc[cp.td], &ac = hd.ac[cp.ta];
-                for (int v = 0; v < cp.v; v++)
-                    for (int h = 0; h < cp.h; h++) {
-                        const int by = my * cp.v + v, bx = mx * cp.h + h;
-                        int16_t *blk = coef + (P.coef_off[c] + (int64_t)by * P.bw[c] + bx) * 64;
-                        const int s = decode(bits, dc);
-                        if (s > 11) fail("bad DC category");
-                        pred[c] += s ? extend(bits.get(s), s) : 0;
-                        blk[0] = (int16_t)pred[c];
-                        for (int k = 1; k < 64;) {
-                            const int rs = decode(bits, ac);
-                            const int r = rs >> 4, sz = rs & 15;
-                            if (sz) {
-                                k += r;
-                                if (k > 63) fail("AC index out of range");
-                                blk[ZIGZAG[k]] = (int16_t)extend(bits.get(sz), sz);
-                                k++;
-                            } else {
-                                if (r != 15) break;
-                                k += 16;
-                            }
-                        }
-                    }
-            }
-        }
+        entropy_decode(hd, P, jpeg, len, dec->h_coef);
         hipStream_t st = (hipStream_t)hip_stream;
-        if (hipMemcpyAsync(dec->d_coef, coef, (size_t)blocks * 128, hipMemcpyHostToDevice, st) != hipSuccess ||
+        if (hipMemcpyAsync(dec->d_coef, dec->h_coef, (size_t)blocks * 128, hipMemcpyHostToDevice, st) != hipSuccess ||
             hipEventRecord(dec->staged, st) != hipSuccess)
             return err(ZR_ERR_DEVICE, "jpeg: coefficient upload failed");
         P.coef = dec->d_coef;
         P.planes = dec->d_planes;
-        P.W = hd.W;
-        P.H = hd.H;
-        P.hs = hd.ncomp == 3 ? hd.comp[0].h : 1;
-        P.vs = hd.ncomp == 3 ? hd.comp[0].v : 1;
-        P.cw = hd.ncomp == 3 ? (hd.W + P.hs - 1) / P.hs : 0;  // downsampled_width (jdinput.c)
-        P.ch = hd.ncomp == 3 ? (hd.H + P.vs - 1) / P.vs : 0;
         P.out = d_rgba;
         P.out_stride = (int64_t)row_stride;
         zr::launch_jpeg(P, st);

@@ -16,6 +16,27 @@ def info(data: bytes):
     return w.value, h.value
 
 
+class _Layout(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("ncomp", C.c_uint32),
+                ("h_samp", C.c_uint32), ("v_samp", C.c_uint32), ("total_blocks", C.c_uint32),
+                ("bw", C.c_uint32 * 3), ("bh", C.c_uint32 * 3), ("qsel", C.c_uint32 * 3),
+                ("quant", (C.c_uint16 * 64) * 4)]
+
+
+def coefficients(data: bytes):
+    """Host-only entropy decoding (no GPU): (layout dict, int16 [total_blocks, 64] quantised
+    coefficients in natural order, components concatenated)."""
+    import numpy as np
+    lay = _Layout()
+    check(lib().zr_jpeg_coefficients(data, len(data), None, 0, C.byref(lay)))
+    coef = np.empty((lay.total_blocks, 64), np.int16)
+    check(lib().zr_jpeg_coefficients(data, len(data), coef.ctypes.data, lay.total_blocks, C.byref(lay)))
+    d = {k: getattr(lay, k) for k in ("width", "height", "ncomp", "h_samp", "v_samp", "total_blocks")}
+    d["bw"], d["bh"], d["qsel"] = list(lay.bw), list(lay.bh), list(lay.qsel)
+    d["quant"] = np.array([list(r) for r in lay.quant], np.uint16)
+    return d, coef
+
+
 class JpegDecoder:
     """A reusable decoder (zr_jpeg_decoder): coefficient staging and planes grow on demand."""
 
