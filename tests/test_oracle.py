@@ -202,6 +202,14 @@ for m, s in sizes.items():
     n = O.Net(f"{sys.argv[1]}/zaru_amd/models/{m}.onnx", f64=False)
     for k in range(2):
         n.run(np.random.default_rng(k).uniform(-1, 1, (1, 3, s, s)).astype(np.float32))
+import io
+from PIL import Image
+from zaru_amd import jpeg
+for shape, sub in (((37, 53, 3), 2), ((40, 24, 3), 1), ((16, 16, 3), 0), ((21, 30), 0)):
+    b = io.BytesIO()
+    Image.fromarray(np.random.default_rng(1).integers(0, 256, size=shape, dtype=np.uint8)).save(
+        b, "JPEG", quality=80, subsampling=sub)
+    O.jpeg_pixels(*reversed(jpeg.coefficients(b.getvalue())))
 print("clean")
 """
 
@@ -218,7 +226,8 @@ def test_oracle_interpreter_is_memory_clean(tmp_path):
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     lib = str(tmp_path / "liboracle_asan.so")
     subprocess.run(["gcc", "-shared", "-fPIC", "-O1", "-g", "-fsanitize=address", "-fno-omit-frame-pointer",
-                    "-ffp-contract=off", "-o", lib, f"{repo}/oracle/geom.c", f"{repo}/oracle/nnexec.c", "-lm"],
+                    "-ffp-contract=off", "-o", lib, f"{repo}/oracle/geom.c", f"{repo}/oracle/nnexec.c",
+                    f"{repo}/oracle/jpeg.c", "-lm"],
                    check=True)
     env = dict(os.environ, LD_PRELOAD=asan, ASAN_OPTIONS="detect_leaks=0")
     r = subprocess.run([sys.executable, "-c", ASAN_CHILD, repo, lib], env=env, capture_output=True,
