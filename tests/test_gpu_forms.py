@@ -39,8 +39,9 @@ SWITCHES = {
     "no_v4": "-v4,-dma",
     "no_rows": "-rows",
     "no_vres": "-vres",
+    "no_vstore": "-vstore",
     "chain": "+chain",  # low-resolution layer runs in one launch per image (chain.hip)
-    "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres",
+    "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore",
 }
 
 

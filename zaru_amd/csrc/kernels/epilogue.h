@@ -21,14 +21,14 @@ __device__ __forceinline__ int mfma32_row(int r, int kh) { return (r & 3) + 8 * 
 
 // One 32x32 accumulator tile of one lane: rows mbase + mfma32_row(r, kh), column (n, q).
 // Loads (bias, residual, slopes) are all issued before any is used, from clamped addresses:
-// the tile pays one memory latency, not sixteen.
-__device__ __forceinline__ void epilogue_tile(const GemmParams &P, const f32x16 &acc, int n, int q,
-                                              int mbase, int kh) {
+// the tile pays one memory latency, not sixteen.  epilogue_values leaves the 16 results in v;
+// epilogue_tile also stores them.
+__device__ __forceinline__ void epilogue_values(const GemmParams &P, const f32x16 &acc, int n, int q,
+                                                int mbase, int kh, float v[16]) {
     auto chan = [&](int r) {
         const int m = mbase + mfma32_row(r, kh);
         return m < P.Mpad ? m : 0;
     };
-    float v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = acc[r] + P.bias[chan(r)];
     float rv[16];
@@ -57,6 +57,12 @@ __device__ __forceinline__ void epilogue_tile(const GemmParams &P, const f32x16 
         for (int r = 0; r < 16; ++r) v[r] += rv[r];
     }
     apply_act_n<16>(P.post, v, chan);
+}
+
+__device__ __forceinline__ void epilogue_tile(const GemmParams &P, const f32x16 &acc, int n, int q,
+                                              int mbase, int kh) {
+    float v[16];
+    epilogue_values(P, acc, n, q, mbase, kh, v);
     const uint32_t ob = (uint32_t)n * (uint32_t)P.o_sN + (uint32_t)q * (uint32_t)P.o_sP;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {

@@ -103,8 +103,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmParams P) {
 // i.e. on the same XCD under round-robin dispatch, so their shared X tile is an L2 hit.
 constexpr int TKC = 16;  // K rows per stage
 
+// vec: the output tile leaves through LDS as 16-byte row segments (a wave's 32x32 tile in 4
+// dwordx4 store instructions instead of 16 dword ones) -- the host sets it when a 4-column group
+// never straddles an image and every row segment is 16-B aligned (o_sP == 1, P % 4 == 0, ...).
 template <int MT, int NT>
-__global__ __launch_bounds__(256) void gemm_tiled_kernel(const GemmParams P, int mblocks, int nct) {
+__global__ __launch_bounds__(256) void gemm_tiled_kernel(const GemmParams P, int mblocks, int nct, int vec) {
     constexpr int BN = 4 * NT * 32, MR = MT * 32;
     constexpr int XV = TKC * BN / 4 / 256;  // float4 of X staged per thread per chunk
     constexpr int WV = (TKC * MR / 4 + 255) / 256;
@@ -189,6 +192,36 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const GemmParams P, int
         __syncthreads();
     }
 
+    if (vec) {
+        // the loop's last barrier released sX: each wave takes 32x32 floats of it (BN >= 128)
+        float *sT = &sX[0][0][0] + wave * 1024;
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+            const int jt = j0 + (wave * NT + u) * 32;
+            const int j = min(jt + col, P.ncols - 1);
+            const int n = j / P.P, q = j - n * P.P;
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                float v[16];
+                epilogue_values(P, acc[t][u], n, q, m0 + t * 32, kh, v);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sT[mfma32_row(r, kh) * 32 + col] = v[r];
+                __builtin_amdgcn_wave_barrier();  // LDS ops of a wave complete in order
+                const int c4 = lane & 7, jj = jt + 4 * c4;
+                const int nn = jj / P.P, qq = jj - nn * P.P;
+#pragma unroll
+                for (int it = 0; it < 4; ++it) {
+                    const int rr = it * 8 + (lane >> 3), m = m0 + t * 32 + rr;
+                    const float4 x = *reinterpret_cast<const float4 *>(sT + rr * 32 + 4 * c4);
+                    if (jj < P.ncols && m < P.M)
+                        *reinterpret_cast<float4 *>(P.out + (uint32_t)nn * (uint32_t)P.o_sN + (uint32_t)qq +
+                                                    (uint32_t)m * (uint32_t)P.o_sC) = x;
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < NT; ++u) {
         const int j = j0 + (wave * NT + u) * 32 + col;
@@ -281,7 +314,10 @@ static const char *launch_tiled(const GemmParams &p, hipStream_t s) {
     const int nct = (p.ncols + BN - 1) / BN;
     const int mblocks = (p.Mpad + MT * 32 - 1) / (MT * 32);
     const int nblk = mblocks == 1 ? nct : ((nct + 7) / 8) * 8 * mblocks;
-    hipLaunchKernelGGL((gemm_tiled_kernel<MT, NT>), dim3(nblk), dim3(256), 0, s, p, mblocks, nct);
+    // 16-B output segments: whole 4-column groups inside one image, aligned rows
+    const int vec = form_on(FORM_VSTORE) && p.o_sP == 1 && p.P % 4 == 0 && p.o_sN % 4 == 0 &&
+                    p.o_sC % 4 == 0 && ((uintptr_t)p.out % 16) == 0;
+    hipLaunchKernelGGL((gemm_tiled_kernel<MT, NT>), dim3(nblk), dim3(256), 0, s, p, mblocks, nct, vec);
     static const char *names[2][5] = {
         {"", "gemm_tiled_kernel<1,1>", "gemm_tiled_kernel<2,1>", "gemm_tiled_kernel<3,1>", "gemm_tiled_kernel<4,1>"},
         {"", "gemm_tiled_kernel<1,2>", "gemm_tiled_kernel<2,2>", "gemm_tiled_kernel<3,2>", "gemm_tiled_kernel<4,2>"}};

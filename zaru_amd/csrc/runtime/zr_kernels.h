@@ -242,7 +242,7 @@ struct ChainParams {
 //   valu: VALU dwpw for few-channel high-resolution layers   valu_db: its double-buffered staging
 //   rows: image-row head GEMM (gemm_rows_kernel)   chain: low-resolution layer runs (chain.hip)
 //   vres: VALU dwpw taking the block's residual from the staged depthwise taps
-enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_CHAIN, FORM_VRES, FORM_COUNT };
+enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_CHAIN, FORM_VRES, FORM_VSTORE, FORM_COUNT };
 bool form_on(Form f);
 
 bool stem_supported(int cin, int k, int stride, int cout);
