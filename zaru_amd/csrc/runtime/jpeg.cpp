@@ -184,6 +184,15 @@ struct Bits {
     int cnt = 0;
     bool marker = false;  // a marker was reached: feed zeros (T.81 F.2.2.5 leaves this to us)
     void fill() {
+        // bulk path: 4 bytes at once while none of them is 0xFF (no stuffing, no marker)
+        while (cnt <= 32 && !marker && p + 4 <= n) {
+            const uint32_t x = ((uint32_t)d[p] << 24) | ((uint32_t)d[p + 1] << 16) | ((uint32_t)d[p + 2] << 8) | d[p + 3];
+            const uint32_t t = ~x;
+            if ((t - 0x01010101u) & ~t & 0x80808080u) break;  // some byte is 0xFF
+            acc |= (uint64_t)x << (32 - cnt);
+            cnt += 32;
+            p += 4;
+        }
         while (cnt <= 56) {
             uint32_t b = 0;
             if (!marker && p < n) {
