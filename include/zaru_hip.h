@@ -145,8 +145,9 @@ typedef struct {
 int zr_track_seed_async(zr_track_state *d_state, size_t n, const zr_track_cfg *cfg,
                         zr_view_desc *d_views, void *hip_stream);
 /* Consume the estimate made on d_views (landmark output 0, and output 1 with flag_stride floats
- * per image for kinds 0/1), update the states, write frame-space landmarks to d_lm_out
- * (n x L x 3, may be NULL) and the next views. */
+ * per image for kinds 0/1 -- the flag -- and kind 2 -- the 5 iris points, which come first),
+ * update the states, write frame-space landmarks to d_lm_out (n x L x 3, may be NULL) and the
+ * next views. */
 int zr_track_update_async(zr_track_state *d_state, size_t n, const zr_track_cfg *cfg,
                           const float *d_landmarks, const float *d_flag, size_t flag_stride,
                           float *d_lm_out, zr_view_desc *d_views, void *hip_stream);

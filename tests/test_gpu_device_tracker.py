@@ -36,7 +36,23 @@ CASES = {  # network: onnx, input side, colour lo, oracle kind, padding, loss th
     # the frames hold no hands: loss threshold 0 (LandmarkTracker::set_loss_threshold) keeps the
     # ROIs in the tracked branch so the hand mapping is compared at all
     "hand": ("hand_landmark_lite", 224, 0.0, O.HAND, 0.4, 0.0),
+    # the other extract / angle kinds of track.hip: FaceMesh V2 (478 points, kind 0), the eye
+    # network (no confidence, no angle: kind 2), a 68-point network (relative (x, y): kind 3)
+    "facemesh_v2": ("face_landmarks_detector", 256, -1.0, O.FACEMESH_V2, 0.3, 0.5),
+    "eye": ("iris_landmark", 64, -1.0, None, 0.3, 0.5),
+    "face68_pfld": ("landmarks_68_pfld", 112, 0.0, None, 0.3, 0.5),
 }
+
+
+def extract_positions(network, outs, side):
+    """Each network's extract (mediapipe.rs:59-71,99-114; hand/landmark.rs:298-322; eye.rs:47-64;
+    multipie68.rs:108-117) as n x 3 positions in network-input pixels."""
+    if network == "eye":
+        return np.concatenate([outs[1].reshape(5, 3), outs[0].reshape(71, 3)]).astype(np.float32)
+    if network == "face68_pfld":
+        xy = outs[0].reshape(-1)[:136].reshape(68, 2) * np.float32(side)
+        return np.concatenate([xy, np.zeros((68, 1), np.float32)], 1).astype(np.float32)
+    return outs[0].reshape(-1, 3)
 
 
 def video(n_streams, steps, seed):
@@ -63,23 +79,25 @@ def video(n_streams, steps, seed):
     return frames, rois
 
 
-def oracle_step(net, img, roi, side, lo, kind, pad):
+def oracle_step(net, img, roi, side, lo, kind, pad, network):
     cx, cy, w, h, rad = roi
     vr = O.RRect(O.grow_to_fit_aspect(O.Rect(cx, cy, w, h), 1, 1), rad)
     view = O.view_compose(O.view_full(W, H), vr)
     lrect = O.grow_to_fit_aspect(O.Rect.from_top_left(0, 0, view.rect.w, view.rect.h), 1, 1)
     outs = net.run(O.preproc(img, O.view_compose(view, lrect), side, side, lo, 1.0)[None])
-    conf = O.landmark_confidence(kind, outs)
-    pos = O.estimator_map(outs[0].reshape(-1, 3), lrect, side)
-    est = O.landmark_angle(kind, pos)
+    conf = O.landmark_confidence(kind, outs) if kind is not None else 1.0
+    pos = O.estimator_map(extract_positions(network, outs, side), lrect, side)
+    est = O.landmark_angle(kind, pos) if kind is not None else 0.0  # unwrap_or(0.0)
     lms, upd, nxt = O.tracker_update(pos, vr, rad, est, pad)
     # the estimate angle is well-conditioned only when its two landmarks are apart (as e2e)
+    if kind is None:  # no estimate angle: the ROI keeps its rotation
+        return conf, lms, upd, nxt, lrect.w / side, 1e9
     a, b = (0, 9) if kind == O.HAND else (263, 33)
     sep = float(np.hypot(*(pos[a, :2] - pos[b, :2]))) / (lrect.w / side)
     return conf, lms, upd, nxt, lrect.w / side, sep
 
 
-@pytest.mark.parametrize("network", ["facemesh", "hand"])
+@pytest.mark.parametrize("network", ["facemesh", "hand", "facemesh_v2", "eye", "face68_pfld"])
 def test_device_tracker_follows_oracle(network):
     import zaru_amd.host as Hm
     from zaru_amd._lib import DeviceBuffer
@@ -107,7 +125,8 @@ def test_device_tracker_follows_oracle(network):
             if not active[s]:
                 assert not st[s]["active"] and not st[s]["tracked"]
                 continue
-            conf, want, upd, nxt, per_px, sep = oracle_step(net, frames[t, s], prev[s], side, lo, kind, pad)
+            conf, want, upd, nxt, per_px, sep = oracle_step(net, frames[t, s], prev[s], side, lo, kind, pad,
+                                                            network)
             if abs(conf - loss) < BAND:
                 stats["band"] += 1
                 active[s] = st[s]["active"]
@@ -138,5 +157,5 @@ def test_device_tracker_follows_oracle(network):
     assert stats["band"] == 0
     assert stats["tracked"] >= (S // 2) * T // 2
     assert stats["lm_ok"] >= 0.9 * stats["tracked"]
-    if network == "facemesh":
+    if network in ("facemesh", "facemesh_v2"):
         assert stats["lost"] >= 1  # the noise-only streams lose their ROI (landmark.rs:468-477)

@@ -76,7 +76,7 @@ void DeviceTracker::step(const std::vector<Image> &frames) {
     const ColorMapper cm = cnn_->color_mapper();
     // the frame table is staged (pinned) inside the call, so zf may die after it returns
     check(zr_cnn_estimate_device_views_async(nn.handle(), zf.data(), n_, views_.ptr, n_, cm.lo, cm.hi, outs, stream_));
-    const bool flagged = cfg_.kind == 0 || cfg_.kind == 1;
+    const bool flagged = cfg_.kind <= 2;  // flag output, or (kind 2) the iris output
     check(zr_track_update_async(state_.ptr, n_, &cfg_, outs_[0].ptr, flagged ? outs_[1].ptr : nullptr,
                                 flagged ? (size_t)nn.output_per_image(1) : 0, lm_out_.ptr, views_.ptr, stream_));
 }

@@ -128,7 +128,11 @@ __global__ __launch_bounds__(256) void track_kernel(const TrackParams P) {
             return;
         }
         const int L = P.L;
-        const float *lm = P.lm + (int64_t)i * L * (P.kind == 3 ? 2 : 3);
+        // per-image landmark output 0: L x 3 floats, 2L (kind 3), or the 71-point eye contour
+        // (kind 2, whose 5 iris points come first from output 1, eye.rs:47-64)
+        const int lstride = P.kind == 3 ? 2 * L : P.kind == 2 ? 3 * (L - 5) : 3 * L;
+        const float *lm = P.lm + (int64_t)i * lstride;
+        const float *iris = P.kind == 2 ? P.flag + (int64_t)i * P.flag_stride : nullptr;
         const float scale = st.local[2] / (float)P.in_w;
         // map-out of landmark j (Estimator, landmark.rs:336-345): p * scale, then + rect.x / .y
         auto mapped = [&](int j, float &x, float &y, float &z) {
@@ -136,6 +140,11 @@ __global__ __launch_bounds__(256) void track_kernel(const TrackParams P) {
                 x = lm[2 * j] * (float)P.in_w;
                 y = lm[2 * j + 1] * (float)P.in_h;
                 z = 0.f;
+            } else if (P.kind == 2) {
+                const float *src = j < 5 ? iris + 3 * j : lm + 3 * (j - 5);
+                x = src[0];
+                y = src[1];
+                z = src[2];
             } else {
                 x = lm[3 * j];
                 y = lm[3 * j + 1];

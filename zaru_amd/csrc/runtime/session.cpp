@@ -629,8 +629,10 @@ int zr_track_update_async(zr_track_state *d_state, size_t n, const zr_track_cfg 
     return guarded([&]() -> int {
         zr::TrackParams p{};
         if (int rc = track_params(p, d_state, n, cfg, d_views)) return rc;
-        if (!d_landmarks || ((cfg->kind == 0 || cfg->kind == 1) && (!d_flag || flag_stride == 0)))
+        if (!d_landmarks || (cfg->kind <= 2 && (!d_flag || flag_stride == 0)))
             return set_err(ZR_ERR_INVALID_ARGUMENT, "missing landmark / flag outputs");
+        if (cfg->kind == 2 && (cfg->num_landmarks <= 5 || flag_stride < 15))
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "eye network: output 1 holds the 5 iris points");
         p.lm = d_landmarks;
         p.flag = d_flag;
         p.flag_stride = (int)flag_stride;
