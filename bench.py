@@ -177,7 +177,7 @@ def kernel_symbol(name: str) -> str:
     return name.replace(" ", "")
 
 
-def measure_traffic(args, kind):
+def measure_traffic(args, kind, batch=None):
     """HBM bytes per launch of every kernel symbol, from two rocprofv3 --pmc passes (one counter
     each, no other trace domain) over a short child run of this same benchmark.  Per
     MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are KiB, and on gfx950 FETCH_SIZE counts
@@ -192,7 +192,7 @@ def measure_traffic(args, kind):
     child = [sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
              "--no-cpu-baseline", "--no-profile", "--no-traffic", "--no-hand", "--no-next", "--no-tracking",
              "--no-jpeg",
-             "--batch", str(args.batch), "--workload", kind,
+             "--batch", str(batch or args.batch), "--workload", kind,
              "--sub-batches", str(args.sub_batches), "--streams", args.streams]
     kib, launches = {}, {}
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
@@ -372,9 +372,14 @@ def main():
     primary = args.workload if args.workload in ("hand", "face_next") else "face"
     # child processes first, while this one has not touched the GPU: PMC traffic passes,
     # then the CPU baseline (its workers would otherwise compete with the pipeline's threads)
-    traffic = None
+    traffic, side_traffic = None, {}
     if world == 1 and not args.no_traffic and not args.no_profile:
         traffic = measure_traffic(args, primary)
+        # the side lines' dominant kernels, at the side lines' own batch sizes
+        if args.workload == "face" and not args.no_hand:
+            side_traffic["hand"] = measure_traffic(args, "hand", args.hand_batch)
+        if args.workload == "face" and not args.no_next:
+            side_traffic["face_next"] = measure_traffic(args, "face_next", args.next_batch)
     cpu = None
     if world == 1 and not args.no_cpu_baseline and primary in ("face", "hand"):
         cpu = cpu_baseline(primary, args.cpu_baseline_seconds, args.batch, WORKLOADS[primary][5])
@@ -494,9 +499,9 @@ def main():
         out["roofline"] = roofline_of(kernels, traffic)
         out["kernels"] = sorted(kernels, key=lambda k: -k["ms"])
     if world == 1 and args.workload == "face" and not args.no_hand:
-        out["hand"] = hand_line(H, args, device)
+        out["hand"] = hand_line(H, args, device, side_traffic.get("hand"))
     if world == 1 and args.workload == "face" and not args.no_next:
-        out["face_next"] = next_line(H, args, device)
+        out["face_next"] = next_line(H, args, device, side_traffic.get("face_next"))
     if world == 1 and args.workload == "face" and not args.no_tracking:
         out["tracking"] = tracking_line(H, args, device, wl)
     if world == 1 and args.workload == "face" and not args.no_jpeg:
@@ -511,7 +516,7 @@ NEXT_METRIC = "end-to-end faces/sec (full-range detect + 478-pt FaceMesh V2), 10
 NEXT_WORKLOAD = "SURVEY 8f-1: BlazeFace full range -> FaceMesh V2 face pipeline (config 3 frames)"
 
 
-def next_line(H, args, device):
+def next_line(H, args, device, traffic=None):
     """SURVEY §8f-1 on the same GPU after the face line: BlazeFace full range (192^2, 2304
     anchors) -> FaceMesh V2 (256^2, 478 points) over config 3's frame generator."""
     import torch
@@ -537,7 +542,7 @@ def next_line(H, args, device):
                                  "frac": round(fps * bpf / 1e9 / HBM_PEAK_GBS, 4)}}
     if not args.no_profile:
         kernels, _ = w.profiled(H, 5)
-        out["roofline"] = roofline_of(kernels, None)
+        out["roofline"] = roofline_of(kernels, traffic)
         out["kernels"] = sorted(kernels, key=lambda k: -k["ms"])[:8]
     del w
     return out
@@ -640,7 +645,7 @@ def jpeg_line(args, device, n_distinct=32, n_decodes=512, threads=16):
                                         "note": "Pillow's libjpeg-turbo (the reference's libjpeg-turbo backend), one core"}}
 
 
-def hand_line(H, args, device):
+def hand_line(H, args, device, traffic=None):
     """Config 4 on the same GPU after the face line: palm lite on every frame + hand landmark
     lite on 4 ROIs per frame (detection-derived when the palm detector fires, else seeded
     rotated ROIs).  The frames hold no hands, so the figure is landmark-ROI throughput."""
@@ -660,7 +665,7 @@ def hand_line(H, args, device):
            "frames_per_step": args.hand_batch}
     if not args.no_profile:
         kernels, _ = w.profiled(H, 5)
-        out["roofline"] = roofline_of(kernels, None)
+        out["roofline"] = roofline_of(kernels, traffic)
         out["kernels"] = sorted(kernels, key=lambda k: -k["ms"])[:8]
     del w
     return out
