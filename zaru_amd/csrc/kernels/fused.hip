@@ -723,8 +723,12 @@ __global__ __launch_bounds__(256) void dwpw_vres_kernel(const DwPwParams P, int 
 // next chunk's copy is in flight while this chunk's depthwise (from LDS) and MFMAs run; the
 // barrier that publishes the depthwise tile to the MFMAs is a bare s_barrier, so it does not
 // drain that copy.
+// (MTW == 1: 4 waves per SIMD fit in 128 registers without spills; the hint moves the
+// accumulators out of AGPRs -- 119 VGPRs instead of 119 + 16, i.e. 4 waves instead of 3 when
+// the LDS plan leaves room for a fourth workgroup)
 template <int K, int S, int WM, int MTW, int DFKC>
-__global__ __launch_bounds__(256) void dwpw_dma_kernel(const DwPwParams P, int nct, int runmax, int bufsz) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTW == 1 ? 4 : 1)))
+void dwpw_dma_kernel(const DwPwParams P, int nct, int runmax, int bufsz) {
     constexpr int WN = 4 / WM, BN = WN * 32, BM = WM * MTW * 32, KK = K * K;
     constexpr int CPAR = 256 / BN, PER = DFKC / CPAR;
     constexpr int KKP = (DFKC * KK + 3) / 4 * 4;
