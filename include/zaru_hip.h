@@ -111,8 +111,9 @@ int zr_detection_candidates_async(const float *d_logits, const float *d_boxes, u
  * zr_track_update_async consumes that estimate: loss check, map-out, angle, transform_out,
  * RotatedRect::bounding, grow_rel(padding), and the next view.  ROI i is evaluated on frame i
  * of each step's frame array.  Geometry follows the host restatement operation for operation
- * (f32, no contraction); cos/sin/atan2/exp are the device's (<= 2 ulp from glibc), so results
- * match the host path within tolerance, not bit for bit. */
+ * (f32, no contraction) with glibc 2.35's own sinf/cosf/expf/atan2f restated on the device
+ * (verified over every f32 input), so the update and the view table are bit-identical to the
+ * host path given the same network outputs. */
 typedef struct {
     float roi[5];       /* RotatedRect {cx, cy, w, h, rad} tracked next (LandmarkTracker::roi) */
     float view_rect[5]; /* roi.grow_to_fit_aspect(aspect) of the pending estimate */
@@ -144,13 +145,18 @@ typedef struct {
 /* Derive every state's first view from state.roi (LandmarkTracker::set_roi); no estimate. */
 int zr_track_seed_async(zr_track_state *d_state, size_t n, const zr_track_cfg *cfg,
                         zr_view_desc *d_views, void *hip_stream);
-/* Consume the estimate made on d_views (landmark output 0, and output 1 with flag_stride floats
- * per image for kinds 0/1 -- the flag -- and kind 2 -- the 5 iris points, which come first),
- * update the states, write frame-space landmarks to d_lm_out (n x L x 3, may be NULL) and the
- * next views. */
+/* Consume the estimate made on d_views (landmark output 0 with lm_stride floats per image, and
+ * output 1 with flag_stride floats per image for kinds 0/1 -- the flag -- and kind 2 -- the 5
+ * iris points, which come first), update the states, write frame-space landmarks to d_lm_out
+ * (n x L x 3, may be NULL; rows of ROIs not tracked this step are NaN) and the next views.
+ * lm_stride must cover what the kind's extract reads (3L; 2L for kind 3; 3(L-5) for kind 2). */
 int zr_track_update_async(zr_track_state *d_state, size_t n, const zr_track_cfg *cfg,
-                          const float *d_landmarks, const float *d_flag, size_t flag_stride,
-                          float *d_lm_out, zr_view_desc *d_views, void *hip_stream);
+                          const float *d_landmarks, size_t lm_stride, const float *d_flag,
+                          size_t flag_stride, float *d_lm_out, zr_view_desc *d_views, void *hip_stream);
+/* The sampling parameters the preprocessing derives from each zr_view: glibc cosf/sinf of the
+ * angle (rect.rs:135-137,417-423), so a caller can build or check a device view table.  A view
+ * whose frame index is past the call's frame table samples Color::NONE everywhere. */
+int zr_view_describe(const zr_view *views, size_t n, uint32_t frame, zr_view_desc *out);
 /* Cnn::estimate (nn/mod.rs:118-126) with a device-resident view table (frames: host array). */
 int zr_cnn_estimate_device_views_async(zr_session *s, const zr_frame *frames, size_t n_frames,
                                        const zr_view_desc *d_views, size_t n_views, float lo,
@@ -197,6 +203,10 @@ int zr_profile_read(zr_session *s, char *buf, size_t cap, size_t *needed);
  * `*needed` receives the full length + 1. */
 int zr_plan_describe(const uint8_t *onnx, size_t len, const uint32_t *out_sel, size_t n_sel,
                      char *buf, size_t cap, size_t *needed);
+
+/* Test hook: evaluate the device restatement of glibc's sinf (fn 0), cosf (1), expf (2),
+ * atanf (3) or atan2f(a, b) (4) on n device floats (kernels/glibc_math.h). */
+int zr_debug_glibc_math(int fn, const float *d_a, const float *d_b, float *d_out, size_t n, void *hip_stream);
 
 /* Thread-local text of the last error (anyhow::Error text). */
 const char *zr_last_error(void);

@@ -8,11 +8,12 @@ grow_to_fit_aspect + ViewData::view (image/mod.rs:201-210), preprocessing, the f
 extract, Estimator map-out (landmark.rs:336-345), the loss check, angle, transform_out and
 RotatedRect::bounding + grow_rel (rect.rs:84-93,287-325).
 
-Tolerances are the e2e test's (SURVEY §8a iii and tests/test_gpu_e2e.py) except that the
-device builds the sampling views itself, with the device's cosf/sinf (<= 2 ulp from glibc):
-a nearest sample sitting on a rounding boundary may then move to the neighbouring pixel, so
-landmarks are held to L2 <= 1e-3 network px on at least 90 % of the tracked ROIs and to
-LM_MAX_PX on all of them.
+The device builds the next step's sampling views itself (kernels/track.hip, with glibc's own
+sinf/cosf/atan2f/expf restated in kernels/glibc_math.h): after every step the device view table
+must be byte-identical to the view the host path (Estimator / pipeline.cpp + make_view) derives
+from the device's new ROI, so the preprocessing is bit-exact (SURVEY §8a iv) and landmarks are
+held to the e2e bar on every tracked ROI: L2 <= 1e-3 network px (SURVEY §8a iii).  Rows of
+ROIs that are not tracked are NaN.
 """
 import math
 import os
@@ -28,7 +29,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MODELS = os.path.join(REPO, "zaru_amd", "models")
 W, H = 640, 480
 BAND = 1e-5
-LM_TOL, LM_MAX_PX = 1e-3, 0.05
+LM_TOL = 1e-3
 CONF_TOL, ANGLE_TOL, RECT_TOL = 1e-4, 2e-4, 2e-2
 
 CASES = {  # network: onnx, input side, colour lo, oracle kind, padding, loss threshold
@@ -41,6 +42,9 @@ CASES = {  # network: onnx, input side, colour lo, oracle kind, padding, loss th
     "facemesh_v2": ("face_landmarks_detector", 256, -1.0, O.FACEMESH_V2, 0.3, 0.5),
     "eye": ("iris_landmark", 64, -1.0, None, 0.3, 0.5),
     "face68_pfld": ("landmarks_68_pfld", 112, 0.0, None, 0.3, 0.5),
+    # the other 68-point network: its output 0 is wider than the 136 floats the extract reads
+    # (multipie68.rs:71,108), so the track kernel's per-image stride must come from the network
+    "face68_peppa": ("slim_160_latest", 160, -1.0, None, 0.3, 0.5),
 }
 
 
@@ -49,7 +53,7 @@ def extract_positions(network, outs, side):
     multipie68.rs:108-117) as n x 3 positions in network-input pixels."""
     if network == "eye":
         return np.concatenate([outs[1].reshape(5, 3), outs[0].reshape(71, 3)]).astype(np.float32)
-    if network == "face68_pfld":
+    if network in ("face68_pfld", "face68_peppa"):
         xy = outs[0].reshape(-1)[:136].reshape(68, 2) * np.float32(side)
         return np.concatenate([xy, np.zeros((68, 1), np.float32)], 1).astype(np.float32)
     return outs[0].reshape(-1, 3)
@@ -97,7 +101,7 @@ def oracle_step(net, img, roi, side, lo, kind, pad, network):
     return conf, lms, upd, nxt, lrect.w / side, sep
 
 
-@pytest.mark.parametrize("network", ["facemesh", "hand", "facemesh_v2", "eye", "face68_pfld"])
+@pytest.mark.parametrize("network", ["facemesh", "hand", "facemesh_v2", "eye", "face68_pfld", "face68_peppa"])
 def test_device_tracker_follows_oracle(network):
     import zaru_amd.host as Hm
     from zaru_amd._lib import DeviceBuffer
@@ -109,16 +113,22 @@ def test_device_tracker_follows_oracle(network):
     fb = H * W * 4
     tr = Hm.DeviceTracker(network, 0, pad, loss)
     tr.set_rois(rois, [(W, H)] * S)
+    seeded = tr.views()
+    for s in range(S):
+        want = tr.host_view(Hm.RotatedRect(Hm.Rect.from_center(*rois[s][:4]), rois[s][4]), W, H, s)
+        assert (seeded[s].view(np.uint32) == want.view(np.uint32)).all(), (network, s, seeded[s], want)
     net = O.Net(os.path.join(MODELS, model + ".onnx"), f64=False)
     prev = [tuple(r) for r in rois]
     active = [True] * S
     skip = set()
-    stats = {"tracked": 0, "lost": 0, "band": 0, "lm_ok": 0, "lm_max": 0.0, "rect": 0.0, "ang": 0.0}
+    stats = {"tracked": 0, "lost": 0, "band": 0, "lm_ok": 0, "lm_max": 0.0, "rect": 0.0, "ang": 0.0,
+             "views_equal": 0}
     for t in range(T):
         tr.step([(buf.ptr + (t * S + s) * fb, W, H, W * 4) for s in range(S)])
         tr.synchronize()
         st = tr.states()
         lms = tr.landmarks()
+        views = tr.views()
         for s in range(S):
             if s in skip:
                 continue
@@ -135,14 +145,19 @@ def test_device_tracker_follows_oracle(network):
             assert st[s]["tracked"] == (conf >= loss), (network, t, s, conf)
             if not st[s]["tracked"]:
                 assert not st[s]["active"]
+                assert np.isnan(lms[s]).all(), (network, t, s)
                 active[s] = False
                 stats["lost"] += 1
                 continue
             stats["tracked"] += 1
+            # the view the next step samples == the host path's view of the new ROI, bytewise
+            hv = tr.host_view(st[s]["roi"], W, H, s)
+            assert (views[s].view(np.uint32) == hv.view(np.uint32)).all(), (network, t, s, views[s], hv)
+            stats["views_equal"] += 1
             l2 = float(np.sqrt(((lms[s][:, :2] - want[:, :2]) ** 2).sum(-1)).max()) / per_px
             stats["lm_max"] = max(stats["lm_max"], l2)
             stats["lm_ok"] += int(l2 <= LM_TOL)
-            assert l2 <= LM_MAX_PX, (network, t, s, l2)
+            assert l2 <= LM_TOL, (network, t, s, l2)
             for got, w in ((st[s]["updated_roi"], upd), (st[s]["roi"], nxt)):
                 d_ang = abs(got.rotation_radians() - w.rad)
                 d_px = max(abs(a - b) for a, b in zip(got.rect().tuple(), w.rect.tuple())) / per_px
@@ -156,6 +171,6 @@ def test_device_tracker_follows_oracle(network):
     print(network, stats)
     assert stats["band"] == 0
     assert stats["tracked"] >= (S // 2) * T // 2
-    assert stats["lm_ok"] >= 0.9 * stats["tracked"]
+    assert stats["lm_ok"] == stats["tracked"] == stats["views_equal"]
     if network in ("facemesh", "facemesh_v2"):
         assert stats["lost"] >= 1  # the noise-only streams lose their ROI (landmark.rs:468-477)

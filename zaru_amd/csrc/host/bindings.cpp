@@ -328,6 +328,19 @@ PYBIND11_MODULE(_zaru_host, m) {
             }
             return out;
         })
+        .def("views", [](DeviceTracker &t) {
+            auto v = t.views();
+            py::array_t<float> a({(py::ssize_t)v.size(), (py::ssize_t)10});
+            static_assert(sizeof(zr_view_desc) == 40, "zr_view_desc");
+            std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(zr_view_desc));
+            return a;  // f32 view of {half_w, half_h, tl_x, tl_y, view_w, view_h, cos, sin, frame, pad}
+        })
+        .def("host_view", [](const DeviceTracker &t, const RotatedRect &roi, uint32_t fw, uint32_t fh, uint32_t frame) {
+            const zr_view_desc d = t.host_view(roi, fw, fh, frame);
+            py::array_t<float> a(10);
+            std::memcpy(a.mutable_data(), &d, sizeof(d));
+            return a;
+        })
         .def("landmarks", [](DeviceTracker &t) {
             auto v = t.landmarks();
             py::array_t<float> a({(py::ssize_t)t.size(), (py::ssize_t)t.network().num_landmarks, (py::ssize_t)3});

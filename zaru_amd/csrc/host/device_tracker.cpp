@@ -77,8 +77,9 @@ void DeviceTracker::step(const std::vector<Image> &frames) {
     // the frame table is staged (pinned) inside the call, so zf may die after it returns
     check(zr_cnn_estimate_device_views_async(nn.handle(), zf.data(), n_, views_.ptr, n_, cm.lo, cm.hi, outs, stream_));
     const bool flagged = cfg_.kind <= 2;  // flag output, or (kind 2) the iris output
-    check(zr_track_update_async(state_.ptr, n_, &cfg_, outs_[0].ptr, flagged ? outs_[1].ptr : nullptr,
-                                flagged ? (size_t)nn.output_per_image(1) : 0, lm_out_.ptr, views_.ptr, stream_));
+    check(zr_track_update_async(state_.ptr, n_, &cfg_, outs_[0].ptr, (size_t)nn.output_per_image(0),
+                                flagged ? outs_[1].ptr : nullptr, flagged ? (size_t)nn.output_per_image(1) : 0,
+                                lm_out_.ptr, views_.ptr, stream_));
 }
 
 void DeviceTracker::synchronize() {
@@ -92,6 +93,28 @@ std::vector<zr_track_state> DeviceTracker::states() {
         synchronize();
     }
     return h;
+}
+
+std::vector<zr_view_desc> DeviceTracker::views() {
+    std::vector<zr_view_desc> h(n_);
+    if (n_) {
+        check(zr_memcpy_async(h.data(), views_.ptr, n_ * sizeof(zr_view_desc), 1, stream_));
+        synchronize();
+    }
+    return h;
+}
+
+zr_view_desc DeviceTracker::host_view(const RotatedRect &roi, uint32_t frame_w, uint32_t frame_h,
+                                      uint32_t frame) const {
+    // LandmarkTracker::track_impl's view (landmark.rs:465-467) + Estimator's aspect fit
+    // (landmark.rs:320-323), as the host pipeline builds it (pipeline.cpp)
+    const AspectRatio a = cnn_->aspect();
+    const ViewData view = ViewData::full(frame_w, frame_h).view(roi.grow_to_fit_aspect(a));
+    const ViewData net = view.view(RotatedRect(view.local_rect().grow_to_fit_aspect(a), 0.f));
+    const zr_view z = to_zr_view(net);
+    zr_view_desc d{};
+    check(zr_view_describe(&z, 1, frame, &d));
+    return d;
 }
 
 std::vector<float> DeviceTracker::landmarks() {

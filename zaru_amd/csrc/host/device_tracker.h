@@ -27,7 +27,10 @@ class DeviceTracker {
     size_t size() const { return n_; }
     const LandmarkNetwork &network() const { return net_; }
     std::vector<zr_track_state> states();      // after synchronize()
-    std::vector<float> landmarks();            // last step, frame px, n x L x 3
+    std::vector<float> landmarks();            // last step, frame px, n x L x 3 (NaN rows: not tracked)
+    std::vector<zr_view_desc> views();         // the view table the next step samples
+    // the view the host path (pipeline.cpp / Estimator) derives from `roi`, for parity checks
+    zr_view_desc host_view(const RotatedRect &roi, uint32_t frame_w, uint32_t frame_h, uint32_t frame) const;
     void *stream() const { return stream_; }
 
   private:

@@ -36,7 +36,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const StemParams P) {
         // all of this thread's pixel gathers are issued before the first is used
         constexpr int NP = (RIN * WIN + 255) / 256;
         const ViewDesc d = P.pre.views[n];
-        const FrameDesc f = P.pre.frames[d.frame];
+        const FrameDesc f = frame_of(P.pre, d);
         uint32_t px[NP];
         bool pad[NP];
 #pragma unroll

@@ -14,7 +14,7 @@ __global__ __launch_bounds__(256) void preproc_kernel(const PreprocParams P) {
     if (q >= P.OW * P.OH) return;
     const int y = q / P.OW, x = q - y * P.OW;
     const ViewDesc d = P.views[v];
-    const FrameDesc f = P.frames[d.frame];
+    const FrameDesc f = frame_of(P, d);
     const uint32_t rgba = sample_view(d, f, x, y, P.OW, P.OH);
     float *o = P.out + (int64_t)v * P.o_sN + q;
     o[0] = color_map(rgba, 0, P.adjust, P.lo);

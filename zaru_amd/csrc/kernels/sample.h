@@ -44,6 +44,16 @@ __device__ __forceinline__ int64_t sample_offset(const ViewDesc &d, const FrameD
     return (int64_t)((uint64_t)iy * f.stride + (uint64_t)ix * 4);
 }
 
+// The frame a view samples.  Device-built view tables (zr_cnn_estimate_device_views_async) are
+// not range-checked on the host: an index past the frame table samples a 0x0 frame (every
+// pixel Color::NONE) through frame 0's valid pointer instead of reading past the table.
+__device__ __forceinline__ FrameDesc frame_of(const PreprocParams &P, const ViewDesc &d) {
+    const bool ok = d.frame < (uint32_t)P.nframes;
+    FrameDesc f = P.frames[ok ? d.frame : 0];
+    if (!ok) f.w = f.h = 0;
+    return f;
+}
+
 // Load of a sampled pixel without a branch around the load (Color::NONE = 0 for -1).
 __device__ __forceinline__ uint32_t load_pixel(const FrameDesc &f, int64_t off) {
     const uint32_t v = *(const uint32_t *)(f.rgba + (off >= 0 ? off : 0));

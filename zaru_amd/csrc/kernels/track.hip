@@ -9,9 +9,11 @@
 //   4. next RoI = grow_rel(padding) (landmark.rs:493), and from it the next estimate's view
 //      exactly as the host builds it (grow_to_fit_aspect, ViewData::view twice,
 //      image/mod.rs:201-210, nn/mod.rs:118-126), written as the preprocessing's view table.
-// f32 throughout, no contraction (HIPFLAGS -ffp-contract=off), Rust's operation order; the only
-// departures from the host restatement are the device cosf / sinf / atan2f / expf (<= 2 ulp).
+// f32 throughout, no contraction (HIPFLAGS -ffp-contract=off), Rust's operation order, and
+// glibc's own sinf / cosf / atan2f / expf (glibc_math.h, verified over every f32 input), so the
+// update and the view table it writes are bit-identical to the host restatement.
 #include "../runtime/zr_track.h"
+#include "glibc_math.h"
 
 namespace zr {
 namespace {
@@ -24,14 +26,14 @@ struct RRect {  // Rect as (centre, size) (rect.rs:15-18) + rotation
 };
 
 __device__ __forceinline__ V2 rot_ccw(V2 v, float r) {  // matrix.rs:571-579, ops.rs:68-77
-    const float c = cosf(r), s = sinf(r), ns = -s;
+    const float c = glibc::cosf(r), s = glibc::sinf(r), ns = -s;
     return {(0.f + c * v.x) + ns * v.y, (0.f + s * v.x) + c * v.y};
 }
 
 __device__ __forceinline__ float signed_angle_to(V2 a, V2 b) {  // vector.rs:568-573
     const float perp = a.x * b.y - a.y * b.x;
     const float dot = (0.f + a.x * b.x) + a.y * b.y;
-    return -atan2f(perp, dot);
+    return -glibc::atan2f(perp, dot);
 }
 
 __device__ __forceinline__ RRect from_top_left(float x, float y, float w, float h, float rad) {
@@ -91,8 +93,8 @@ __device__ void next_view(TrackState &st, ViewDesc &vd, int frame, int aw, int a
     vd.tl_y = net.cy - net.h * 0.5f;
     vd.view_w = net.w;
     vd.view_h = net.h;
-    vd.cos_r = cosf(net.rad);
-    vd.sin_r = sinf(net.rad);
+    vd.cos_r = glibc::cosf(net.rad);
+    vd.sin_r = glibc::sinf(net.rad);
     vd.frame = (uint32_t)frame;
     vd.pad_ = 0;
 }
@@ -106,6 +108,14 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// Landmark rows of a ROI that is not tracked this step (lost now or earlier) hold NaN, so a
+// reader that ignores states()[i].tracked cannot mistake a stale estimate for a result.
+__device__ void invalidate_rows(const TrackParams &P, int i, int tid) {
+    if (!P.lm_out) return;
+    float *q = P.lm_out + (int64_t)i * P.L * 3;
+    for (int j = tid; j < 3 * P.L; j += 256) q[j] = __builtin_nanf("");
+}
+
 __global__ __launch_bounds__(256) void track_kernel(const TrackParams P) {
     const int i = blockIdx.x, tid = threadIdx.x;
     if (i >= P.n) return;  // whole workgroup
@@ -113,13 +123,15 @@ __global__ __launch_bounds__(256) void track_kernel(const TrackParams P) {
     TrackState st = P.state[i];
     if (!P.seed) {
         if (!st.active) {  // lost earlier: stays lost (roi = None)
+            invalidate_rows(P, i, tid);
             if (tid == 0) P.state[i].tracked = 0;
             return;
         }
         float conf = 1.f;
-        if (P.kind == 0) conf = 1.f / (1.f + expf(-P.flag[(int64_t)i * P.flag_stride]));  // num.rs:6-8
+        if (P.kind == 0) conf = 1.f / (1.f + glibc::expf(-P.flag[(int64_t)i * P.flag_stride]));  // num.rs:6-8
         else if (P.kind == 1) conf = P.flag[(int64_t)i * P.flag_stride];
         if (conf < P.loss_thresh) {
+            invalidate_rows(P, i, tid);
             if (tid == 0) {
                 P.state[i].active = 0;
                 P.state[i].tracked = 0;
@@ -128,10 +140,10 @@ __global__ __launch_bounds__(256) void track_kernel(const TrackParams P) {
             return;
         }
         const int L = P.L;
-        // per-image landmark output 0: L x 3 floats, 2L (kind 3), or the 71-point eye contour
-        // (kind 2, whose 5 iris points come first from output 1, eye.rs:47-64)
-        const int lstride = P.kind == 3 ? 2 * L : P.kind == 2 ? 3 * (L - 5) : 3 * L;
-        const float *lm = P.lm + (int64_t)i * lstride;
+        // per-image landmark output 0 (lm_stride floats per image, checked on the host to hold
+        // L x 3, 2L for kind 3, or the 71-point eye contour for kind 2, whose 5 iris points come
+        // first from output 1, eye.rs:47-64)
+        const float *lm = P.lm + (int64_t)i * P.lm_stride;
         const float *iris = P.kind == 2 ? P.flag + (int64_t)i * P.flag_stride : nullptr;
         const float scale = st.local[2] / (float)P.in_w;
         // map-out of landmark j (Estimator, landmark.rs:336-345): p * scale, then + rect.x / .y
@@ -167,7 +179,7 @@ __global__ __launch_bounds__(256) void track_kernel(const TrackParams P) {
         }
         const float angle = st.roi[4] + est;
         const RRect vr = {st.view_rect[0], st.view_rect[1], st.view_rect[2], st.view_rect[3], st.view_rect[4]};
-        const float c = cosf(-angle), s = sinf(-angle), ns = -s;  // rect.rs:287-325
+        const float c = glibc::cosf(-angle), s = glibc::sinf(-angle), ns = -s;  // rect.rs:287-325
         float mnx = 3.40282347e38f, mny = 3.40282347e38f, mxx = -3.40282347e38f, mxy = -3.40282347e38f;
         for (int j = tid; j < L; j += 256) {
             float x, y, z;
@@ -232,6 +244,28 @@ __global__ __launch_bounds__(256) void track_kernel(const TrackParams P) {
 const char *launch_track(const TrackParams &p, hipStream_t s) {
     hipLaunchKernelGGL(track_kernel, dim3(p.n), dim3(256), 0, s, p);
     return "track_kernel";
+}
+
+// Test hook (zr_debug_glibc_math): the device evaluation of glibc_math.h, one thread per input.
+__global__ __launch_bounds__(256) void glibc_math_kernel(int fn, const float *a, const float *b, float *out,
+                                                         int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float x = a[i];
+    float r;
+    switch (fn) {
+        case 0: r = glibc::sinf(x); break;
+        case 1: r = glibc::cosf(x); break;
+        case 2: r = glibc::expf(x); break;
+        case 3: r = glibc::atanf(x); break;
+        default: r = glibc::atan2f(x, b[i]); break;
+    }
+    out[i] = r;
+}
+
+const char *launch_glibc_math(int fn, const float *a, const float *b, float *out, int64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(glibc_math_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, fn, a, b, out, n);
+    return "glibc_math_kernel";
 }
 
 }  // namespace zr

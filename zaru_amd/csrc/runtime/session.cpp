@@ -544,6 +544,7 @@ static int views_common(zr_session *s, Ctx *c, const zr_frame *frames, size_t nf
     if (int rc = upload_views(c, frames, nf, views, view_frame, d_views ? 0 : nv, stream)) return rc;
     zr::PreprocParams p{};
     p.frames = c->frames;
+    p.nframes = (int)nf;
     p.views = d_views ? d_views : c->views;
     p.nviews = (int)nv;
     p.OW = s->plan.in_W;
@@ -624,8 +625,8 @@ int zr_track_seed_async(zr_track_state *d_state, size_t n, const zr_track_cfg *c
 }
 
 int zr_track_update_async(zr_track_state *d_state, size_t n, const zr_track_cfg *cfg, const float *d_landmarks,
-                          const float *d_flag, size_t flag_stride, float *d_lm_out, zr_view_desc *d_views,
-                          void *hip_stream) {
+                          size_t lm_stride, const float *d_flag, size_t flag_stride, float *d_lm_out,
+                          zr_view_desc *d_views, void *hip_stream) {
     return guarded([&]() -> int {
         zr::TrackParams p{};
         if (int rc = track_params(p, d_state, n, cfg, d_views)) return rc;
@@ -633,11 +634,40 @@ int zr_track_update_async(zr_track_state *d_state, size_t n, const zr_track_cfg 
             return set_err(ZR_ERR_INVALID_ARGUMENT, "missing landmark / flag outputs");
         if (cfg->kind == 2 && (cfg->num_landmarks <= 5 || flag_stride < 15))
             return set_err(ZR_ERR_INVALID_ARGUMENT, "eye network: output 1 holds the 5 iris points");
+        // what each kind's extract reads of output 0 (mediapipe.rs:59-71, hand/landmark.rs:298-322,
+        // eye.rs:47-64, multipie68.rs:71,108: outputs[0][..NUM_LANDMARKS * 2])
+        const size_t L = (size_t)cfg->num_landmarks;
+        const size_t need = cfg->kind == 3 ? 2 * L : cfg->kind == 2 ? 3 * (L - 5) : 3 * L;
+        if (lm_stride < need || lm_stride > (size_t)INT32_MAX)
+            return set_err(ZR_ERR_SHAPE, "landmark output holds fewer floats per image than the extract reads");
         p.lm = d_landmarks;
+        p.lm_stride = (int)lm_stride;
         p.flag = d_flag;
         p.flag_stride = (int)flag_stride;
         p.lm_out = d_lm_out;
         zr::launch_track(p, (hipStream_t)hip_stream);
+        HIP_TRY(hipGetLastError());
+        return ZR_OK;
+    });
+}
+
+int zr_view_describe(const zr_view *views, size_t n, uint32_t frame, zr_view_desc *out) {
+    return guarded([&]() -> int {
+        if (!views || !out) return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument");
+        for (size_t i = 0; i < n; i++) {
+            const zr::ViewDesc d = make_view(views[i], frame);
+            std::memcpy(&out[i], &d, sizeof(d));
+        }
+        return ZR_OK;
+    });
+}
+
+int zr_debug_glibc_math(int fn, const float *d_a, const float *d_b, float *d_out, size_t n, void *hip_stream) {
+    return guarded([&]() -> int {
+        if (fn < 0 || fn > 4 || !d_a || !d_out || (fn == 4 && !d_b) || n > (size_t)INT64_MAX / 2)
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "bad glibc-math request");
+        if (n == 0) return ZR_OK;
+        zr::launch_glibc_math(fn, d_a, d_b, d_out, (int64_t)n, (hipStream_t)hip_stream);
         HIP_TRY(hipGetLastError());
         return ZR_OK;
     });
@@ -715,6 +745,7 @@ int zr_preprocess_views_async(const zr_frame *frames, size_t n_frames, const zr_
         HIP_TRY(hipMemcpyAsync(df, fd.data(), n_frames * sizeof(zr::FrameDesc), hipMemcpyHostToDevice, st));
         zr::PreprocParams p{};
         p.frames = df;
+        p.nframes = (int)n_frames;
         p.views = dv;
         p.nviews = (int)n_views;
         p.OW = (int)ow;

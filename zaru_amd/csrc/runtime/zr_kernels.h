@@ -130,6 +130,7 @@ struct PreprocParams {
     const FrameDesc *frames;
     const ViewDesc *views;
     int nviews, OW, OH;
+    int nframes;             // a view whose frame index is >= nframes samples Color::NONE
     float lo, adjust;        // ColorMapper: c * adjust + lo
     float *out;              // (view v, channel c, position q) at out + v*o_sN + c*o_sC + q
     int64_t o_sN, o_sC;

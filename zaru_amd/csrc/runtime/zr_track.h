@@ -29,6 +29,7 @@ struct TrackParams {
     const float *flag;     // output 1: n x flag_stride (face_flag logit / presence); null: kind 2/3
     float *lm_out;         // out: frame-space landmarks, n x L x 3 (may be null)
     int n, L, flag_stride;
+    int lm_stride;         // floats per image of output 0
     int kind;              // 0 FaceMesh (sigmoid flag, eyes 33->263 vs +X), 1 hand (presence, 0->9 vs +Y),
                            // 2 no confidence / no angle (eye), 3 as 2 with (x, y) relative pairs (68-point)
     int in_w, in_h;        // network input (map-out scale, kind 3 coordinate scale)
@@ -38,5 +39,7 @@ struct TrackParams {
 };
 
 const char *launch_track(const TrackParams &p, hipStream_t s);
+// fn: 0 sinf, 1 cosf, 2 expf, 3 atanf, 4 atan2f(a, b) -- glibc_math.h on the device
+const char *launch_glibc_math(int fn, const float *a, const float *b, float *out, int64_t n, hipStream_t s);
 
 }  // namespace zr
