@@ -147,3 +147,62 @@ def test_record_gather_overlaps_steps_world2_gloo():
                                *[c for kp in d.keypoints() for c in kp]))
                         for d in _frame_detections(H, f)][:8]
                 assert recs[1000 * k + f] == want
+
+
+def _combined_worker(rank, world, port, steps, q):
+    """Config 5's gather: each step packs the face pipeline's records and the hand pipeline's
+    palm records of the rank's frames into one [2B, W] block (bench.py run_steps: face ids
+    rank + world*i, hand ids rank + world*(B + i)) and ships both in the one collective."""
+    import torch.distributed as dist
+    import zaru_amd.host as H
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        B = 5
+        g = shard.RecordGather(2 * B, shard.record_width(), "cpu")
+        got = []
+        for k in range(steps):
+            face_ids = [rank + world * i for i in range(B)]
+            hand_ids = [rank + world * (B + i) for i in range(B)]
+            face = H.pack_detection_records([_frame_detections(H, 100 * k + f)[:3] for f in face_ids],
+                                            face_ids, 8)
+            palm = H.pack_detection_records([_frame_detections(H, 5000 + 100 * k + f) for f in hand_ids],
+                                            hand_ids, 8)
+            g.submit(np.concatenate([face, palm]))
+            got.append(None)
+        g.finish()
+        got = [g.result(k).numpy().copy() for k in range(max(0, steps - 2), steps)]
+        q.put((rank, got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_combined_face_palm_gather_world2_gloo():
+    world, steps, B = 2, 4, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_combined_worker, args=(r, world, port, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import zaru_amd.host as H
+
+    def tup(d):
+        return tuple(float(np.float32(v)) for v in (d.confidence(), d.angle(), *d.bounding_rect().tuple(),
+                                                     *[c for kp in d.keypoints() for c in kp]))
+    for rank in range(world):
+        for j, k in enumerate(range(steps - 2, steps)):
+            blk = results[rank][j]
+            assert blk.shape == (world * 2 * B, shard.record_width())
+            assert np.array_equal(blk, results[0][j])
+            recs = shard.unpack_records(blk)
+            assert sorted(recs) == list(range(2 * B * world))  # every face and hand frame of every rank
+            for fid, dets in recs.items():
+                src = (100 * k + fid) if fid < B * world else (5000 + 100 * k + fid)
+                want = [tup(d) for d in _frame_detections(H, src)]
+                want = want[:3] if fid < B * world else want[:8]
+                assert dets == want, (rank, k, fid)
