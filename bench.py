@@ -97,6 +97,10 @@ def parse():
     ap.add_argument("--tracking-steps", type=int, default=50)
     ap.add_argument("--no-jpeg", action="store_true", help="skip the SURVEY §8f-2 JPEG-source line at N = 1")
     ap.add_argument("--next-batch", type=int, default=512)
+    ap.add_argument("--no-c5", action="store_true", help="skip the config-5 line (face + hand concurrently) at N = 1")
+    ap.add_argument("--c5-steps", type=int, default=8)
+    ap.add_argument("--prime-seconds", type=float, default=0.6,
+                    help="untimed pipeline priming before the warmup steps (see prime())")
     return ap.parse_args()
 
 
@@ -191,7 +195,7 @@ def measure_traffic(args, kind, batch=None):
         return None
     child = [sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
              "--no-cpu-baseline", "--no-profile", "--no-traffic", "--no-hand", "--no-next", "--no-tracking",
-             "--no-jpeg",
+             "--no-jpeg", "--no-c5",
              "--batch", str(batch or args.batch), "--workload", kind,
              "--sub-batches", str(args.sub_batches), "--streams", args.streams]
     kib, launches = {}, {}
@@ -270,13 +274,25 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(kind, seconds, batch, seed):
+def cpu_quota():
+    """CPUs this process may really use: the cgroup v2 quota (cpu.max), else its affinity."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, round(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_baseline(kind, seconds, batch, seed, P=None):
     """The reference path restated on the host (oracle/cpu_baseline.py): P single-threaded
     worker processes (ORT's 1 intra + 1 inter thread per session, nn/mod.rs:342-346) over the
-    bench's own frames, P = the cores this process may use (at most 16, the per-GPU CPU share
-    of the GPU box).  Runs before this process touches the GPU."""
+    bench's own frames; P = nproc by default (one instance per host core).
+    Runs before this process touches the GPU."""
     import subprocess
-    P = max(1, min(16, len(os.sched_getaffinity(0))))
+    P = P or os.cpu_count() or 1
     env = dict(os.environ, OMP_NUM_THREADS="1")
     cmd = [sys.executable, os.path.join(REPO, "oracle", "cpu_baseline.py"), "--workload", kind,
            "--workers", str(P), "--seconds", str(seconds), "--batch", str(batch), "--seed", str(seed)]
@@ -293,7 +309,8 @@ def cpu_baseline(kind, seconds, batch, seed):
     stage = {k: round(sum(r["stage_ms"][k] for r in res) / max(1, frames), 3) for k in res[0]["stage_ms"]}
     value = sum(r["tracked"] / r["seconds"] for r in res)
     return {"value": round(value, 2), "unit": "faces/s" if kind == "face" else "tracked hands/s",
-            "cores": len(res), "kind": "port",
+            "cores": len(res), "kind": "port", "processes": P, "nproc": os.cpu_count(),
+            "cpu_quota": cpu_quota(),
             "rois_per_s": round(sum(r["rois"] / r["seconds"] for r in res), 2),
             "frames_per_s": round(sum(r["frames"] / r["seconds"] for r in res), 2),
             "cpu": cpu_model(), "stage_ms_per_frame": stage,
@@ -341,6 +358,22 @@ class Workload:
         return parse_profile(txt), p.times()
 
 
+def prime(workloads, seconds, pool):
+    """Untimed steps before the warmup, until `seconds` have passed (at least 3 steps): the
+    first launches of every kernel load their code objects and the GPU leaves its idle clocks,
+    which makes the first ~10 steps up to 2.3x slower than steady state
+    (profiles/r03_probe_steps.jsonl).  The W warmup and K timed steps follow unchanged."""
+    import torch
+    t0 = time.perf_counter()
+    n = 0
+    while n < 3 or time.perf_counter() - t0 < seconds:
+        run_steps(workloads, 1, None, 0, 1, pool)
+        n += 1
+    torch.cuda.synchronize()
+    return {"steps": n, "seconds": round(time.perf_counter() - t0, 3),
+            "why": "first-launch code-object loads and GPU clock ramp before the warmup steps"}
+
+
 def run_steps(workloads, steps, gather, rank, world, pool):
     """`steps` software-pipelined steps of every workload (concurrently when there are two),
     each step's detection records all-gathered asynchronously (world > 1)."""
@@ -382,7 +415,12 @@ def main():
             side_traffic["face_next"] = measure_traffic(args, "face_next", args.next_batch)
     cpu = None
     if world == 1 and not args.no_cpu_baseline and primary in ("face", "hand"):
-        cpu = cpu_baseline(primary, args.cpu_baseline_seconds, args.batch, WORKLOADS[primary][5])
+        seed = WORKLOADS[primary][5]
+        cpu = cpu_baseline(primary, args.cpu_baseline_seconds, args.batch, seed)
+        if cpu is not None and (os.cpu_count() or 1) > 16:  # the GPU box's per-GPU CPU share
+            c16 = cpu_baseline(primary, args.cpu_baseline_seconds, args.batch, seed, P=16)
+            if c16 is not None:
+                cpu["p16"] = {k: c16[k] for k in ("value", "cores", "frames_per_s", "sample")}
 
     import torch
     import torch.distributed as dist
@@ -410,6 +448,7 @@ def main():
         from concurrent.futures import ThreadPoolExecutor
         pool = ThreadPoolExecutor(len(wls))
 
+    primed = prime(wls, args.prime_seconds, pool)
     run_steps(wls, args.warmup, gather, rank, world, pool)
     if world > 1:
         dist.barrier()
@@ -471,7 +510,9 @@ def main():
                    "frames_per_gpu_per_step": args.batch, "frame": "1920x1080 RGBA8",
                    "sub_batches": args.sub_batches, "streams": args.streams,
                    "parallelism": f"frame-sharded x{world}"
-                   + (", one async RCCL all-gather of detection records per step" if world > 1 else "")},
+                   + ((", one async gloo all-gather of detection records per step (shared-GPU dry run)" if share
+                       else ", one async RCCL all-gather of detection records per step") if world > 1 else "")},
+        "prime": primed,
         "frames_per_s": round(frames / elapsed, 1),
         "rois_per_s": round(rois / elapsed, 1),
         "tracked_per_step": round(tracked / args.steps / world, 2),
@@ -504,6 +545,8 @@ def main():
         out["face_next"] = next_line(H, args, device, side_traffic.get("face_next"))
     if world == 1 and args.workload == "face" and not args.no_tracking:
         out["tracking"] = tracking_line(H, args, device, wl)
+    if world == 1 and args.workload == "face" and not args.no_c5:
+        out["config5"] = c5_line(H, args, device, wl)
     if world == 1 and args.workload == "face" and not args.no_jpeg:
         out["jpeg_source"] = jpeg_line(args, device)
     out["cpu_baseline"] = cpu
@@ -643,6 +686,39 @@ def jpeg_line(args, device, n_distinct=32, n_decodes=512, threads=16):
             "jpeg_MB_per_frame": round(mb, 3), "quality": 90, "subsampling": "4:2:0",
             "cpu_libjpeg_turbo_1core": {"value": round(cpu_n / cpu_el, 1), "unit": "frames/s",
                                         "note": "Pillow's libjpeg-turbo (the reference's libjpeg-turbo backend), one core"}}
+
+
+def c5_line(H, args, device, wl):
+    """Config 5 on one GPU: the face pipeline (config 3, the main line's own)
+    and a hand pipeline (config 4: palm lite + 4 hand ROIs per frame) over the SAME resident
+    1080p frames, each stepping from its own host thread on its own HIP streams
+    (examples/facemesh.rs:35-56 and examples/hand_tracking.rs:19-62 sharing the GPU).  At N > 1
+    the same pair runs per rank with one combined record all-gather (--workload both)."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    threads = max(2, args.threads // 2)
+    face = Workload(H, "face", device, args.batch, 0, threads, args.sub_batches, args.streams == "multi",
+                    shared=wl)
+    hand = Workload(H, "hand", device, args.batch, 0, threads, args.sub_batches, args.streams == "multi",
+                    shared=wl)
+    pool = ThreadPoolExecutor(2)
+    prime([face, hand], 0.3, pool)
+    run_steps([face, hand], 2, None, 0, 1, pool)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tf, th = run_steps([face, hand], args.c5_steps, None, 0, 1, pool)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    pool.shutdown()
+    del face, hand
+    return {"metric": "config 5 on one GPU: face pipeline + hand pipeline concurrently over the same 1080p frames",
+            "faces_per_s": round(tf["tracked"] / el, 1), "hand_rois_per_s": round(th["rois"] / el, 1),
+            "frames_per_s": round(tf["frames"] / el, 1), "frames_per_step": args.batch,
+            "steps": args.c5_steps, "ms_per_step": round(1e3 * el / args.c5_steps, 3),
+            "rois_per_frame": {"face": round(tf["rois"] / max(1, tf["frames"]), 3),
+                               "hand": round(th["rois"] / max(1, th["frames"]), 3)},
+            "streams": "each pipeline: its own host thread and sub-batch HIP streams",
+            "multi_gpu": "bench.py --workload both: per rank, one combined face+palm record all-gather per step"}
 
 
 def hand_line(H, args, device, traffic=None):

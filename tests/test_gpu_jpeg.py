@@ -87,6 +87,34 @@ def test_decoder_reuse_across_sizes(dec):
         assert np.array_equal(dec.decode(data), libjpeg_turbo_rgba(data))
 
 
+def test_one_decoder_alternating_streams(dec):
+    """One decoder, consecutive frames enqueued on two different streams without a host wait
+    between them (INTEGRATION.md §8's per-frame stream pool): the second frame's coefficient
+    upload must not overwrite buffers the first frame's kernels are still reading."""
+    import ctypes as C
+
+    from zaru_amd._lib import DeviceBuffer, check, lib
+    frames = [synthetic(1080, 1920, 900 + i) for i in range(6)]
+    datas = [encode(f, quality=90) for f in frames]
+    streams = []
+    for _ in range(2):
+        sp = C.c_void_p()
+        check(lib().zr_stream_create(C.byref(sp)))
+        streams.append(sp.value)
+    bufs = [DeviceBuffer(1080 * 1920 * 4) for _ in datas]
+    try:
+        for i, d in enumerate(datas):
+            dec.decode_into(d, bufs[i].ptr, 1920 * 4, streams[i % 2])
+        for s in streams:
+            check(lib().zr_stream_synchronize(s))
+        for i, d in enumerate(datas):
+            got = bufs[i].download((1080, 1920, 4), "uint8")
+            assert np.array_equal(got, libjpeg_turbo_rgba(d)), i
+    finally:
+        for s in streams:
+            lib().zr_stream_destroy(s)
+
+
 def test_decoded_frames_feed_the_pipeline(dec):
     """Frames decoded into HBM by the JPEG source run the config-3 pipeline exactly as frames
     uploaded from libjpeg-turbo's host decode (same bytes -> same detections and landmarks)."""

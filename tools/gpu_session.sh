@@ -14,5 +14,5 @@ timeout -k 10 600 python bench.py "$@" > $O/bench.json 2> $O/bench.err &&
 echo "bench ok" &&
 timeout -k 10 300 python bench.py --workload both --steps 30 --warmup 5 --no-cpu-baseline --no-traffic --no-profile "$@" > $O/bench_both.json 2>> $O/bench.err &&
 echo "both ok" &&
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic --no-hand --no-next --no-tracking --no-jpeg "$@" > $O/bench_prof.json 2>> $O/bench.err &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic --no-hand --no-next --no-tracking --no-jpeg --no-c5 "$@" > $O/bench_prof.json 2>> $O/bench.err &&
 echo "rocprof ok"

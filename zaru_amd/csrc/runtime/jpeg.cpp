@@ -266,6 +266,7 @@ struct zr_jpeg_decoder {
     uint8_t *d_planes = nullptr;
     size_t planes_cap = 0;
     hipEvent_t staged = nullptr;  // the last H2D copy out of h_coef has completed
+    hipEvent_t done = nullptr;    // the last decode's kernels (readers of d_coef / d_planes) completed
 };
 
 namespace {
@@ -375,6 +376,11 @@ int zr_jpeg_decoder_create(int device, zr_jpeg_decoder **out) {
             delete d;
             return err(ZR_ERR_DEVICE, "hipEventCreate failed");
         }
+        if (hipEventCreateWithFlags(&d->done, hipEventDisableTiming) != hipSuccess) {
+            (void)hipEventDestroy(d->staged);
+            delete d;
+            return err(ZR_ERR_DEVICE, "hipEventCreate failed");
+        }
         *out = d;
         return ZR_OK;
     } catch (...) {
@@ -385,7 +391,9 @@ int zr_jpeg_decoder_create(int device, zr_jpeg_decoder **out) {
 void zr_jpeg_decoder_destroy(zr_jpeg_decoder *d) {
     if (!d) return;
     (void)hipEventSynchronize(d->staged);
+    (void)hipEventSynchronize(d->done);
     (void)hipEventDestroy(d->staged);
+    (void)hipEventDestroy(d->done);
     (void)hipHostFree(d->h_coef);
     (void)hipFree(d->d_coef);
     (void)hipFree(d->d_planes);
@@ -454,6 +462,10 @@ int zr_jpeg_decode_async(zr_jpeg_decoder *dec, const uint8_t *jpeg, size_t len, 
         // stage the coefficients: the previous decode's copy out of the staging must be done
         if (hipSetDevice(dec->device) != hipSuccess) return err(ZR_ERR_DEVICE, "hipSetDevice failed");
         if (hipEventSynchronize(dec->staged) != hipSuccess) return err(ZR_ERR_DEVICE, "event sync failed");
+        // growing frees the device buffers: the previous decode's kernels must be done with them
+        if (((size_t)blocks > dec->coef_cap || (size_t)pbytes > dec->planes_cap) &&
+            hipEventSynchronize(dec->done) != hipSuccess)
+            return err(ZR_ERR_DEVICE, "event sync failed");
         if ((size_t)blocks > dec->coef_cap) {
             (void)hipHostFree(dec->h_coef);
             (void)hipFree(dec->d_coef);
@@ -476,7 +488,10 @@ int zr_jpeg_decode_async(zr_jpeg_decoder *dec, const uint8_t *jpeg, size_t len, 
         }
         entropy_decode(hd, P, jpeg, len, dec->h_coef);
         hipStream_t st = (hipStream_t)hip_stream;
-        if (hipMemcpyAsync(dec->d_coef, dec->h_coef, (size_t)blocks * 128, hipMemcpyHostToDevice, st) != hipSuccess ||
+        // d_coef / d_planes are reused: on another stream the previous decode's IDCT and colour
+        // kernels may still read them, so this stream waits for them before overwriting
+        if (hipStreamWaitEvent(st, dec->done, 0) != hipSuccess ||
+            hipMemcpyAsync(dec->d_coef, dec->h_coef, (size_t)blocks * 128, hipMemcpyHostToDevice, st) != hipSuccess ||
             hipEventRecord(dec->staged, st) != hipSuccess)
             return err(ZR_ERR_DEVICE, "jpeg: coefficient upload failed");
         P.coef = dec->d_coef;
@@ -484,7 +499,8 @@ int zr_jpeg_decode_async(zr_jpeg_decoder *dec, const uint8_t *jpeg, size_t len, 
         P.out = d_rgba;
         P.out_stride = (int64_t)row_stride;
         zr::launch_jpeg(P, st);
-        if (hipGetLastError() != hipSuccess) return err(ZR_ERR_DEVICE, "jpeg: kernel launch failed");
+        if (hipGetLastError() != hipSuccess || hipEventRecord(dec->done, st) != hipSuccess)
+            return err(ZR_ERR_DEVICE, "jpeg: kernel launch failed");
         return ZR_OK;
     } catch (const JpegError &e) {
         return err(e.code, e.msg);
