@@ -65,3 +65,34 @@ def test_form_switch_is_bitwise_neutral(outputs, name):
     assert base.keys() == other.keys()
     for k in base:
         assert np.array_equal(base[k], other[k]), (name, k, float(np.abs(base[k] - other[k]).max()))
+
+
+# A full-plane conv with a non-square kernel (x[N,4,3,5] -> Conv 6x4x3x5 -> y[N,6,1,1]) through
+# gemm_kernel<., true> (the image-row form switched off, as for a step with a residual): its
+# im2col walk must wrap ky at the kernel height, not the width.
+NONSQUARE_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + "/tests")
+from test_lib_cpu import _fld, _vfld, _tensor, _value_info
+from zaru_amd.nn import NeuralNetwork
+rng = np.random.default_rng(3)
+w = rng.uniform(-1, 1, (6, 4, 3, 5)).astype(np.float32)
+node = _fld(1, b"x") + _fld(1, b"w") + _fld(2, b"y") + _fld(4, b"Conv")
+graph = (_fld(1, node) + _fld(5, _tensor(b"w", w.shape, 1, w.tobytes())) +
+         _fld(11, _value_info(b"x", [1, 4, 3, 5])) + _fld(12, _value_info(b"y", [1, 6, 1, 1])))
+net = NeuralNetwork.from_onnx(_fld(7, graph)).load()
+x = rng.uniform(-1, 1, (8, 4, 3, 5)).astype(np.float32)
+got = net.estimate(x)[0].reshape(8, 6)
+want = np.einsum("nchw,mchw->nm", x.astype(np.float64), w.astype(np.float64))
+err = float(np.abs(got - want).max())
+assert err < 1e-5, err
+print("nonsquare ok", err)
+"""
+
+
+@pytest.mark.parametrize("forms", ["", "-rows"])
+def test_nonsquare_full_plane_conv(forms):
+    e = dict(os.environ, ZARU_HIP_FORMS=forms)
+    r = subprocess.run([sys.executable, "-c", NONSQUARE_CHILD, REPO], env=e, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]

@@ -37,7 +37,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmParams P) {
     int ci = 0, ky = 0, kx = kh;
     if constexpr (FULLPLANE) {
         const int oy = q / P.out_W, ox = q - oy * P.out_W;
-        xc = P.x + (int64_t)n * P.x_sN + (int64_t)oy * P.pk * P.x_W + ox * P.pk;
+        xc = P.x + (int64_t)n * P.x_sN + (int64_t)oy * P.ph * P.x_W + ox * P.pk;
         ky = kh / P.pk;
         kx = kh - ky * P.pk;
     } else {
@@ -67,12 +67,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmParams P) {
             float v;
             if constexpr (FULLPLANE) {
                 v = xc[k < P.K ? (int64_t)ci * P.x_sC + ky * P.x_W + kx : 0];
-                kx += 2;  // pk >= 2: at most one wrap of kx, then of ky
+                kx += 2;  // pk >= 2: at most one wrap of kx, then of ky (which wraps at ph)
                 const bool wx = kx >= P.pk;
                 kx -= wx ? P.pk : 0;
                 ky += wx ? 1 : 0;
-                const bool wy = ky >= P.pk;
-                ky -= wy ? P.pk : 0;
+                const bool wy = ky >= P.ph;
+                ky -= wy ? P.ph : 0;
                 ci += wy ? 1 : 0;
             } else {
                 v = xc[(int64_t)kcl * P.x_sC];

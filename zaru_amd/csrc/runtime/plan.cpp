@@ -1349,6 +1349,7 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook
             g.KK = s.KK;
             g.x_sK = 1;
             g.pk = s.kw;
+            g.ph = s.kh;
             g.x_W = s.in.W;
             g.P = s.out.H * s.out.W;
             g.ncols = b.N * g.P;

@@ -38,9 +38,10 @@ struct GemmParams {
     int64_t x_sN, x_sC;
     int KK, x_sK;
     // KK > 1 im2col addressing (gemm_kernel<., true>): k = ci*KK + ky*pk + kx reads
-    // x[ci*x_sC + (oy*pk + ky)*x_W + ox*pk + kx] for output q = oy*out_W + ox -- full-plane
-    // convs (pk = kernel width = plane width, one output) and non-overlapping patches
-    int pk, x_W;
+    // x[ci*x_sC + (oy*ph + ky)*x_W + ox*pk + kx] for output q = oy*out_W + ox -- full-plane
+    // convs (ph x pk = the plane, one output; ph may differ from pk) and non-overlapping
+    // patches (ph == pk)
+    int pk, ph, x_W;
     int P, ncols;        // positions per image, N*P
     int M, K;            // Cout, reduction length (Cin*KK)
     int Mpad, Kpad;      // weights zero-padded to multiples of 32 / 8
