@@ -308,9 +308,11 @@ def cpu_baseline(kind, seconds, batch, seed, P=None):
     frames = sum(r["frames"] for r in res)
     stage = {k: round(sum(r["stage_ms"][k] for r in res) / max(1, frames), 3) for k in res[0]["stage_ms"]}
     value = sum(r["tracked"] / r["seconds"] for r in res)
+    # cores: the hardware threads the P processes really ran on (on the GPU box nproc shows the
+    # whole machine, but the cgroup quota is the per-GPU share)
     return {"value": round(value, 2), "unit": "faces/s" if kind == "face" else "tracked hands/s",
-            "cores": len(res), "kind": "port", "processes": P, "nproc": os.cpu_count(),
-            "cpu_quota": cpu_quota(),
+            "cores": min(len(res), cpu_quota()), "kind": "port", "processes": len(res),
+            "nproc": os.cpu_count(), "cpu_quota": cpu_quota(),
             "rois_per_s": round(sum(r["rois"] / r["seconds"] for r in res), 2),
             "frames_per_s": round(sum(r["frames"] / r["seconds"] for r in res), 2),
             "cpu": cpu_model(), "stage_ms_per_frame": stage,
@@ -420,7 +422,7 @@ def main():
         if cpu is not None and (os.cpu_count() or 1) > 16:  # the GPU box's per-GPU CPU share
             c16 = cpu_baseline(primary, args.cpu_baseline_seconds, args.batch, seed, P=16)
             if c16 is not None:
-                cpu["p16"] = {k: c16[k] for k in ("value", "cores", "frames_per_s", "sample")}
+                cpu["p16"] = {k: c16[k] for k in ("value", "cores", "processes", "frames_per_s", "sample")}
 
     import torch
     import torch.distributed as dist
