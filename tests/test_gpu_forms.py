@@ -40,9 +40,8 @@ SWITCHES = {
     "no_rows": "-rows",
     "no_vres": "-vres",
     "no_vstore": "-vstore",
-    "no_ws": "-ws",
     "chain": "+chain",  # low-resolution layer runs in one launch per image (chain.hip)
-    "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws",
+    "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore",
 }
 
 

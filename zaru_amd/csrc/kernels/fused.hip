@@ -1052,7 +1052,6 @@ const char *launch_dwpw(const DwPwParams &p, hipStream_t s) {
         if (p.k == 3) return p.stride == 1 ? dwpw_valu_co<3, 1>(p, s) : dwpw_valu_co<3, 2>(p, s);
         return p.stride == 1 ? dwpw_valu_co<5, 1>(p, s) : dwpw_valu_co<5, 2>(p, s);
     }
-    if (const char *k = launch_dwpw_ws(p, s)) return k;
     constexpr int64_t min_wgs = 1024;  // workgroups one launch should reach
     const DwPwLayout *best = nullptr;
     int64_t best_wgs = 0;

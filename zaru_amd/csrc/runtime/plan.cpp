@@ -479,8 +479,7 @@ bool Compiler::lower_conv(const OnnxNode &nd) {
         s.K = Cin * s.KK;
         s.Mpad = (int)round_up(Mo, 32);
         s.Kpad = (int)round_up(s.K, 2);
-        // zero rows up to a multiple of 32: dwpw_ws_kernel loads whole 32-row chunks unguarded
-        std::vector<float> wt((size_t)round_up(s.Kpad, 32) * s.Mpad, 0.f);
+        std::vector<float> wt((size_t)s.Kpad * s.Mpad, 0.f);
         for (int m = 0; m < Mo; m++)
             for (int k = 0; k < s.K; k++) wt[(size_t)k * s.Mpad + m] = w->f[(size_t)m * s.K + k];
         s.w_off = push_weights(wt);
@@ -555,7 +554,7 @@ bool Compiler::lower_gemm_node(const OnnxNode &nd) {
     s.K = K;
     s.Mpad = (int)round_up(Mo, 32);
     s.Kpad = (int)round_up(K, 2);
-    std::vector<float> wt((size_t)round_up(s.Kpad, 32) * s.Mpad, 0.f);  // see the Conv case
+    std::vector<float> wt((size_t)s.Kpad * s.Mpad, 0.f);
     for (int k = 0; k < K; k++)
         for (int m = 0; m < Mo; m++)
             wt[(size_t)k * s.Mpad + m] = alpha * (tb ? bm->f[(size_t)m * K + k] : bm->f[(size_t)k * Mo + m]);

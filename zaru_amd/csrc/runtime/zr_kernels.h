@@ -244,9 +244,7 @@ struct ChainParams {
 //   valu: VALU dwpw for few-channel high-resolution layers   valu_db: its double-buffered staging
 //   rows: image-row head GEMM (gemm_rows_kernel)   chain: low-resolution layer runs (chain.hip)
 //   vres: VALU dwpw taking the block's residual from the staged depthwise taps
-//   ws: weight-stationary persistent MFMA dwpw (dwpw_ws_kernel, the low-resolution blocks)
-enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_CHAIN, FORM_VRES, FORM_VSTORE, FORM_WS,
-                  FORM_COUNT };
+enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_CHAIN, FORM_VRES, FORM_VSTORE, FORM_COUNT };
 bool form_on(Form f);
 
 bool stem_supported(int cin, int k, int stride, int cout);
@@ -268,7 +266,6 @@ const char *launch_preproc(const PreprocParams &p, hipStream_t s);
 const char *launch_candidates(const CandParams &p, hipStream_t s);
 const char *launch_stem(const StemParams &p, bool pre, hipStream_t s);
 const char *launch_dwpw(const DwPwParams &p, hipStream_t s);
-const char *launch_dwpw_ws(const DwPwParams &p, hipStream_t s);  // nullptr: form not applicable
 const char *launch_chain(const ChainParams &p, hipStream_t s);
 
 }  // namespace zr
