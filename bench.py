@@ -99,6 +99,9 @@ def parse():
     ap.add_argument("--next-batch", type=int, default=512)
     ap.add_argument("--no-c5", action="store_true", help="skip the config-5 line (face + hand concurrently) at N = 1")
     ap.add_argument("--c5-steps", type=int, default=8)
+    ap.add_argument("--host-post", action="store_true",
+                    help="decode/NMS/map and the tracker update on host threads (the host restatement) "
+                         "instead of on the device")
     ap.add_argument("--prime-seconds", type=float, default=0.6,
                     help="untimed pipeline priming before the warmup steps (see prime())")
     return ap.parse_args()
@@ -195,7 +198,7 @@ def measure_traffic(args, kind, batch=None):
         return None
     child = [sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
              "--no-cpu-baseline", "--no-profile", "--no-traffic", "--no-hand", "--no-next", "--no-tracking",
-             "--no-jpeg", "--no-c5",
+             "--no-jpeg", "--no-c5"] + (["--host-post"] if args.host_post else []) + [
              "--batch", str(batch or args.batch), "--workload", kind,
              "--sub-batches", str(args.sub_batches), "--streams", args.streams]
     kib, launches = {}, {}
@@ -326,6 +329,8 @@ def cpu_baseline(kind, seconds, batch, seed, P=None):
 class Workload:
     """One DetectTrackPipeline over its resident synthetic frames."""
 
+    device_post = True  # bench.py --host-post sets False
+
     def __init__(self, H, kind, device, batch, rank, threads, sub_batches, multi_stream, shared=None):
         det, lm, din, lin, rois, seed = WORKLOADS[kind]
         self.kind, self.batch, self.det, self.lm = kind, batch, det, lm
@@ -343,13 +348,14 @@ class Workload:
         self.args = (base, device, threads, rois, sub_batches)
         self.nets = {"detector": dnet, "landmarker": lnet}
         self.pipe = H.DetectTrackPipeline(base, device, threads, rois, sub_batches, multi_stream,
-                                          **self.nets)
+                                          device_post=Workload.device_post, **self.nets)
         self.pipe.set_frames(self.flist, forced)
 
     def profiled(self, H, steps):
         """Per-kernel HIP-event times with the sub-batches on one stream (uncontended)."""
         kind, device, threads, rois, sub_batches = self.args
-        p = H.DetectTrackPipeline(kind, device, threads, rois, sub_batches, False, **self.nets)
+        p = H.DetectTrackPipeline(kind, device, threads, rois, sub_batches, False,
+                                  device_post=Workload.device_post, **self.nets)
         p.set_frames(self.flist, self.forced)
         p.run_frames_repeated(2)
         p.profile_read()
@@ -401,6 +407,7 @@ def run_steps(workloads, steps, gather, rank, world, pool):
 
 def main():
     args = parse()
+    Workload.device_post = not args.host_post
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

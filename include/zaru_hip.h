@@ -104,6 +104,26 @@ int zr_detection_candidates_async(const float *d_logits, const float *d_boxes, u
                                   uint32_t anchors, uint32_t params, float logit_min,
                                   uint32_t cap, int32_t *d_count, float *d_rec, void *hip_stream);
 
+/* ---- Detector::detect_impl after inference, on the device ----------------------------------
+ * extract_outputs + weighted NMS (Average) + map into frame pixels (crates/zaru/src/
+ * detection.rs:231-267, face/detection.rs:96-157, hand/detection.rs:108-179, detection/nms.rs:
+ * 59-145), one wave per frame, bit-exact with the host restatement (glibc expf / atan2f restated
+ * on the device; NMS ties in anchor order).  Per frame: d_count[f] = detections after NMS, the
+ * first dcap of them in d_dets [n][dcap][20] = {conf, angle, cx, cy, w, h, 7 x (kx, ky)} (frame
+ * px, keypoints past the network's zero), and when d_records is not NULL the all-gather record
+ * [n][2 + 20 rmax] = {frame id first_id + f * id_stride (u32 bits), count (u32 bits), the first
+ * rmax detections}. */
+typedef struct {
+    int face;               /* 1 BlazeFace (angle: eye line vs +X), 0 BlazePalm (wrist -> MCP vs +Y) */
+    int anchors, params, keypoints;  /* A, values per anchor (16 / 18), keypoints (6 / 7) */
+    int in_w, in_h;         /* detector input */
+    float thresh, iou;      /* Detector threshold (0.5), NMS IoU threshold (0.3) */
+} zr_detpost_cfg;
+int zr_detect_post_async(const float *d_logits, const float *d_boxes, const float *d_anchors,
+                         const float *d_letterbox, size_t n, const zr_detpost_cfg *cfg,
+                         int32_t *d_count, float *d_dets, size_t dcap, float *d_records, size_t rmax,
+                         uint32_t first_id, uint32_t id_stride, void *hip_stream);
+
 /* ---- LandmarkTracker state on the device ------------------------------
  * A video loop of LandmarkTracker::track (crates/zaru/src/landmark.rs:463-501) over n streams
  * without a host round trip per frame: the tracker state lives in HBM, the landmark network
@@ -140,6 +160,7 @@ typedef struct {
     int in_w, in_h;     /* network input */
     int aspect_w, aspect_h;
     float loss_thresh, padding;
+    int rois_per_frame; /* ROI i samples frame i / rois_per_frame (0 = 1) */
 } zr_track_cfg;
 
 /* Derive every state's first view from state.roi (LandmarkTracker::set_roi); no estimate. */
@@ -157,6 +178,17 @@ int zr_track_update_async(zr_track_state *d_state, size_t n, const zr_track_cfg 
  * angle (rect.rs:135-137,417-423), so a caller can build or check a device view table.  A view
  * whose frame index is past the call's frame table samples Color::NONE everywhere. */
 int zr_view_describe(const zr_view *views, size_t n, uint32_t frame, zr_view_desc *out);
+/* Seed trackers from device detections (the pipeline's ROI step, pipeline.cpp /
+ * examples/facemesh.rs:49-54, hand/tracking.rs:136-159): ROI slot k of frame f (i = f * R + k,
+ * R = cfg->rois_per_frame) is RotatedRect(det_k.rect[.grow_rel(roi_grow)], roi_use_angle ?
+ * det_k.angle : 0) for the frame's first R detections (NMS order), else -- when the frame has no
+ * detection -- its forced ROI k (d_forced [n][R][5], d_nforced [n]; both may be NULL), else the
+ * slot is idle (active = 0).  Writes the states and their first views (frame f). */
+int zr_track_seed_detections_async(const int32_t *d_count, const float *d_dets, size_t dcap,
+                                   const float *d_forced, const int32_t *d_nforced,
+                                   const uint32_t *d_frame_size, size_t n, const zr_track_cfg *cfg,
+                                   float roi_grow, int roi_use_angle, zr_track_state *d_state,
+                                   zr_view_desc *d_views, void *hip_stream);
 /* Cnn::estimate (nn/mod.rs:118-126) with a device-resident view table (frames: host array). */
 int zr_cnn_estimate_device_views_async(zr_session *s, const zr_frame *frames, size_t n_frames,
                                        const zr_view_desc *d_views, size_t n_views, float lo,

@@ -1,0 +1,79 @@
+"""Detector::detect_impl after inference on the device (zr_detect_post_async, kernels/detpost.hip):
+extract (sigmoid, threshold, decode), weighted NMS and the map into frame pixels
+(crates/zaru/src/detection.rs:231-267, face/detection.rs:96-157, hand/detection.rs:108-179,
+detection/nms.rs:59-145), bit for bit against fixture F3 (tests/golden/decode_cases.npz: raw
+BlazeFace / BlazePalm tensors -> expected detections, pinned by tests/test_host_cpu.py and the
+oracle), all frames of a kind in one launch, plus the all-gather records."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from zaru_amd._lib import DeviceBuffer, check, lib
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+class Cfg(C.Structure):
+    _fields_ = [("face", C.c_int), ("anchors", C.c_int), ("params", C.c_int), ("keypoints", C.c_int),
+                ("in_w", C.c_int), ("in_h", C.c_int), ("thresh", C.c_float), ("iou", C.c_float)]
+
+
+@pytest.mark.parametrize("net", ["face", "palm"])
+def test_detect_post_bit_exact(net):
+    import zaru_amd.host as H
+    g = np.load(os.path.join(GOLDEN, "decode_cases.npz"))
+    keys = sorted({k.split("/")[0] for k in g.files if k.startswith(net)})
+    A, D, nkp, side = (896, 16, 6, 128) if net == "face" else (2016, 18, 7, 192)
+    boxes = np.stack([g[f"{k}/boxes"].reshape(A, D) for k in keys]).astype(np.float32)
+    logits = np.stack([g[f"{k}/confs"].reshape(A) for k in keys]).astype(np.float32)
+    lbox = np.array([H.letterbox_view(*(int(v) for v in g[f"{k}/img"]), side, side)[1].tuple() for k in keys],
+                    np.float32)
+    n, dcap, rmax = len(keys), 32, 8
+    bufs = [DeviceBuffer.from_array(a) for a in (logits, boxes, H.anchors(net).astype(np.float32), lbox)]
+    d_count, d_dets = DeviceBuffer(4 * n), DeviceBuffer(4 * n * dcap * 20)
+    rw = 2 + 20 * rmax
+    d_rec = DeviceBuffer(4 * n * rw)
+    cfg = Cfg(1 if net == "face" else 0, A, D, nkp, side, side, 0.5, 0.3)
+    check(lib().zr_detect_post_async(bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, n, C.byref(cfg),
+                                     d_count.ptr, d_dets.ptr, dcap, d_rec.ptr, rmax, 100, 3, None))
+    count = d_count.download((n,), np.int32)
+    dets = d_dets.download((n, dcap, 20), np.float32)
+    rec = d_rec.download((n, rw), np.float32)
+    for i, k in enumerate(keys):
+        want = g[f"{k}/want"]
+        assert count[i] == len(want), k
+        assert np.array_equal(dets[i, :len(want)].view(np.uint32), want.view(np.uint32)), k
+        # the record: frame id 100 + 3 i, the count, the first rmax detections, zero padding
+        assert rec[i, 0].view(np.uint32) == 100 + 3 * i and rec[i, 1].view(np.uint32) == len(want)
+        m = min(len(want), rmax)
+        assert np.array_equal(rec[i, 2:2 + 20 * m].reshape(m, 20).view(np.uint32), want[:m].view(np.uint32)), k
+        assert not rec[i, 2 + 20 * m:].any()
+
+
+def test_detect_post_empty_and_saturated():
+    """No candidate (every logit low) -> 0 detections; every anchor a candidate (logit high,
+    identical boxes) -> one group of all 896, conf = the seed's."""
+    import zaru_amd.host as H
+    A, D = 896, 16
+    rng = np.random.default_rng(4)
+    boxes = np.tile(rng.uniform(-5, 5, (1, 1, D)).astype(np.float32), (2, A, 1))
+    boxes[:, :, 2:4] = 20.0
+    logits = np.stack([np.full(A, -20.0, np.float32), np.full(A, 8.0, np.float32)])
+    lbox = np.array([H.letterbox_view(640, 480, 128, 128)[1].tuple()] * 2, np.float32)
+    bufs = [DeviceBuffer.from_array(a) for a in (logits, boxes, H.anchors("face").astype(np.float32), lbox)]
+    d_count, d_dets = DeviceBuffer(8), DeviceBuffer(4 * 2 * 4 * 20)
+    cfg = Cfg(1, A, D, 6, 128, 128, 0.5, 0.3)
+    check(lib().zr_detect_post_async(bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, 2, C.byref(cfg),
+                                     d_count.ptr, d_dets.ptr, 4, None, 0, 0, 1, None))
+    count = d_count.download((2,), np.int32)
+    dets = d_dets.download((2, 4, 20), np.float32)
+    want = H.detect_post("face", boxes[1], logits[1], 640, 480)
+    assert count[0] == 0
+    assert count[1] == len(want)
+    for d, w in zip(dets[1], want):
+        assert d[0] == np.float32(w.confidence()) and d[1] == np.float32(w.angle())
+        assert tuple(d[2:6]) == tuple(np.float32(v) for v in w.bounding_rect().tuple())

@@ -181,3 +181,61 @@ def test_repeated_runs_equal_single_run(H):
     for k in range(3):
         p.step(k < 2)
         same()
+
+
+@pytest.mark.parametrize("kind,nets", [("face", {}), ("hand", {}),
+                                       ("face", {"detector": "face_full", "landmarker": "facemesh_v2"})])
+def test_device_post_equals_host_post(H, kind, nets):
+    """The device-resident post-processing (decode + NMS + map, ROI seeding, tracker update on
+    the GPU: PipelineConfig::device_post) gives the host restatement's results bit for bit:
+    detections, seeds, views, tracked flags, confidences, updated / next ROIs, landmarks and the
+    hand extras -- over frames with real faces, noise and forced ROIs, three steps."""
+    from zaru_amd._lib import DeviceBuffer
+    rng = np.random.default_rng(61)
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "sad_linus_mesh.npz"))
+    face = np.repeat(np.repeat(g["codes"][0].transpose(1, 2, 0), 2, axis=0), 2, axis=1)
+    frames = [rng.integers(0, 256, size=(480, 640, 4), dtype=np.uint8) for _ in range(10)]
+    for i in range(0, 10, 2):
+        y, x = int(rng.integers(0, 480 - 384)), int(rng.integers(0, 640 - 384))
+        frames[i][y:y + 384, x:x + 384, :3] = face
+    bufs = [DeviceBuffer.from_array(f) for f in frames]
+    flist = [(b.ptr, 640, 480, 640 * 4) for b in bufs]
+    R = 4 if kind == "hand" else 2
+    forced = [[(float(rng.uniform(150, 490)), float(rng.uniform(150, 330)), float(rng.uniform(120, 300)),
+                float(rng.uniform(120, 300)), float(rng.uniform(-3, 3)) if kind == "hand" else 0.0)
+               for _ in range(R)] for _ in frames]
+
+    def results(device_post):
+        p = H.DetectTrackPipeline(kind, 0, 4, R, 3, True, 0.5 if kind == "face" else 0.0,
+                                  device_post=device_post, **nets)
+        p.set_frames(flist, forced)
+        p.begin_steps()
+        out = []
+        for k in range(3):
+            p.step(k < 2)
+            dets = [[(d.confidence(), d.angle(), d.bounding_rect().tuple(), tuple(d.keypoints())) for d in ds]
+                    for ds in p.detections()]
+            rois = []
+            for i in range(p.num_rois()):
+                r = p.roi(i)
+                row = [r["frame"], r["from_detection"], r["tracked"], r["confidence"], r["roi"].rect().tuple(),
+                       r["roi"].rotation_radians(), r["view_rect"].rect().tuple(), r["view_rect"].rotation_radians()]
+                if r["tracked"]:
+                    row += [r["landmarks"].tobytes(), r["updated_roi"].rect().tuple(),
+                            r["updated_roi"].rotation_radians(), r["next_roi"].rect().tuple()]
+                    for extra in ("raw_handedness", "tongue_out", "world"):
+                        if extra in r:
+                            v = r[extra]
+                            row.append(v.tobytes() if hasattr(v, "tobytes") else v)
+                rois.append(tuple(row))
+            out.append((dets, rois))
+        return out
+
+    host, dev = results(False), results(True)
+    for k in range(3):
+        assert dev[k][0] == host[k][0], ("detections", k)
+        assert len(dev[k][1]) == len(host[k][1])
+        for a, b in zip(dev[k][1], host[k][1]):
+            assert a == b, ("roi", k, a[:4], b[:4])
+    assert any(len(d) for d in host[0][0]) or kind == "hand"
+    assert sum(r[2] for r in host[0][1]) >= 1  # something was tracked

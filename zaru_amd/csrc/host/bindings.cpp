@@ -39,6 +39,9 @@ py::dict estimate_dict(const Estimate &e) {
     d["confidence"] = e.confidence;
     d["raw_handedness"] = e.raw_handedness;
     d["tongue_out"] = e.tongue_out;
+    py::array_t<float> w({(py::ssize_t)(e.world.size() / 3), (py::ssize_t)3});
+    if (!e.world.empty()) std::memcpy(w.mutable_data(), e.world.data(), e.world.size() * 4);
+    d["world"] = w;  // hand metric landmarks (Identity_3); empty for the other networks
     return d;
 }
 
@@ -351,7 +354,7 @@ PYBIND11_MODULE(_zaru_host, m) {
     py::class_<DetectTrackPipeline>(m, "DetectTrackPipeline")
         .def(py::init([](const std::string &kind, int device, int threads, uint32_t max_rois,
                          uint32_t sub_batches, bool stream_per_sub_batch, float loss_threshold,
-                         const std::string &detector, const std::string &landmarker) {
+                         const std::string &detector, const std::string &landmarker, bool device_post) {
                  PipelineConfig c = kind == "hand" ? PipelineConfig::hand() : PipelineConfig::face();
                  if (kind != "hand" && kind != "face")
                      throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "pipeline kind must be 'face' or 'hand'");
@@ -363,12 +366,13 @@ PYBIND11_MODULE(_zaru_host, m) {
                  c.sub_batches = sub_batches;
                  c.stream_per_sub_batch = stream_per_sub_batch;
                  c.loss_threshold = loss_threshold;  // LandmarkTracker::set_loss_threshold
+                 c.device_post = device_post;
                  return new DetectTrackPipeline(c, device, threads);
              }), py::arg("kind") = "face", py::arg("device") = 0, py::arg("threads") = 8,
              py::arg("max_rois_per_frame") = 8, py::arg("sub_batches") = 2,
              py::arg("stream_per_sub_batch") = true,
              py::arg("loss_threshold") = LandmarkTracker::DEFAULT_LOSS_THRESHOLD,
-             py::arg("detector") = "", py::arg("landmarker") = "")
+             py::arg("detector") = "", py::arg("landmarker") = "", py::arg("device_post") = true)
         // frames: list of (device ptr, width, height, row_stride); forced: per frame list of
         // (cx, cy, w, h, rad) ROIs used when the frame has no detection
         .def("run", [](DetectTrackPipeline &p, const std::vector<std::tuple<uint64_t, uint32_t, uint32_t, uint64_t>> &frames,

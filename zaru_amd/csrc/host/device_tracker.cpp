@@ -3,7 +3,6 @@
 
 namespace zh {
 
-namespace {
 int track_kind(NetworkKind k) {
     if (is_face_mesh(k)) return 0;  // face_flag = sigmoid(out1), eye line 33 -> 263
     if (k == NetworkKind::HandLandmarkLite) return 1;
@@ -11,7 +10,6 @@ int track_kind(NetworkKind k) {
     if (k == NetworkKind::FaceOnnx68 || k == NetworkKind::PeppaFacialLandmark68) return 3;
     throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "not a landmark network");
 }
-}  // namespace
 
 DeviceTracker::DeviceTracker(LandmarkNetwork net, int device, float padding, float loss_thresh)
     : net_(net), cnn_(network_cnn(net.kind, device)) {

@@ -11,6 +11,9 @@
 
 namespace zh {
 
+// the track kernel's extract / angle kind of a landmark network (zr_track_cfg::kind)
+int track_kind(NetworkKind k);
+
 class DeviceTracker {
   public:
     DeviceTracker(LandmarkNetwork net, int device = 0, float padding = LandmarkTracker::DEFAULT_ROI_PADDING,

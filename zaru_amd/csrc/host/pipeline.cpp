@@ -105,6 +105,13 @@ DetectTrackPipeline::DetectTrackPipeline(PipelineConfig cfg, int device, int thr
     : cfg_(std::move(cfg)), device_(device), det_cnn_(network_cnn(cfg_.detector.kind, device)),
       lm_cnn_(network_cnn(cfg_.landmarker.kind, device)), pool_(threads) {
     nms_.set_iou_thresh(cfg_.nms_iou);
+    if (cfg_.device_post) {
+        if (cfg_.det_cap < cfg_.max_rois_per_frame) cfg_.det_cap = cfg_.max_rois_per_frame;
+        const auto &a = cfg_.detector.anchors();
+        d_anchors_.resize(2 * a.size());
+        check(zr_memcpy_async(d_anchors_.ptr, a.data(), a.size() * sizeof(Vec2), 0, nullptr));
+        check(zr_stream_synchronize(nullptr));
+    }
     check(zr_stream_create(&stream_));
     // every slot enqueues on the one pipeline stream (the GPU runs the kernels back to back,
     // so per-kernel timings stay clean); the host waits on per-slot events instead
@@ -199,6 +206,7 @@ void DetectTrackPipeline::stage_detect(Slot &s, const std::vector<Image> &frames
     s.d_rec.resize(n * cap * rec_w);
     float *douts[2] = {s.d_boxes.ptr, s.d_logits.ptr};
     dc.estimate_async(s.zf, zv, vf, douts, s.stream);
+    if (cfg_.device_post) return;  // stage_device_post continues on the stream
     check(zr_detection_candidates_async(s.d_logits.ptr, s.d_boxes.ptr, (uint32_t)n, A, D,
                                         candidate_logit_floor(cfg_.det_threshold), cap, s.d_count.ptr,
                                         s.d_rec.ptr, s.stream));
@@ -207,6 +215,200 @@ void DetectTrackPipeline::stage_detect(Slot &s, const std::vector<Image> &frames
     check(zr_memcpy_async(s.h_count.data(), s.d_count.ptr, n * sizeof(int32_t), 1, s.stream));
     check(zr_memcpy_async(s.h_rec.data(), s.d_rec.ptr, n * cap * rec_w * sizeof(float), 1, s.stream));
     check(zr_event_record(s.ev_det, s.stream));
+}
+
+zr_track_cfg DetectTrackPipeline::track_cfg() const {
+    const Cnn &lc = *lm_cnn_;
+    zr_track_cfg c{};
+    c.kind = track_kind(cfg_.landmarker.kind);
+    c.num_landmarks = cfg_.landmarker.num_landmarks;
+    c.in_w = (int)lc.input_width();
+    c.in_h = (int)lc.input_height();
+    c.aspect_w = (int)lc.aspect().w;
+    c.aspect_h = (int)lc.aspect().h;
+    c.loss_thresh = cfg_.loss_threshold;
+    c.padding = cfg_.roi_padding;
+    c.rois_per_frame = (int)std::max(1u, cfg_.max_rois_per_frame);
+    return c;
+}
+
+// device mode, enqueued right behind stage 1 on the slot's stream: decode + NMS + map
+// (zr_detect_post_async), the ROI seeds and their views (zr_track_seed_detections_async), the
+// landmark network on those views and the tracker update (zr_track_update_async), then the
+// results' copies to the host.  ROI slot k of frame f is detection k (NMS order) or, when the
+// frame has none, forced ROI k -- the host mode's seeds -- else idle.
+void DetectTrackPipeline::stage_device_post(Slot &s, const std::vector<Image> &frames,
+                                            const std::vector<std::vector<RotatedRect>> &forced) {
+    const Cnn &dc = *det_cnn_, &lc = *lm_cnn_;
+    const size_t n = s.nf, R = std::max(1u, cfg_.max_rois_per_frame), dcap = cfg_.det_cap;
+    const uint32_t A = (uint32_t)cfg_.detector.anchors().size(), D = (uint32_t)cfg_.detector.params;
+    s.h_lbox.resize(4 * n);
+    s.h_fsize.resize(2 * n);
+    s.h_forced.resize(5 * n * R);
+    s.h_nforced.resize(n);
+    for (size_t i = 0; i < n; i++) {
+        const size_t f = s.f0 + i;
+        const Rect &r = s.letterbox[i];
+        s.h_lbox[4 * i] = r.center().x;
+        s.h_lbox[4 * i + 1] = r.center().y;
+        s.h_lbox[4 * i + 2] = r.width();
+        s.h_lbox[4 * i + 3] = r.height();
+        s.h_fsize[2 * i] = frames[f].width;
+        s.h_fsize[2 * i + 1] = frames[f].height;
+        const size_t nf = f < forced.size() ? std::min(R, forced[f].size()) : 0;
+        s.h_nforced[i] = (int32_t)nf;
+        for (size_t k = 0; k < nf; k++) {
+            const RotatedRect &q = forced[f][k];
+            float *o = &s.h_forced[5 * (i * R + k)];
+            o[0] = q.rect().center().x;
+            o[1] = q.rect().center().y;
+            o[2] = q.rect().width();
+            o[3] = q.rect().height();
+            o[4] = q.rotation_radians();
+        }
+    }
+    s.d_lbox.resize(4 * n);
+    s.d_fsize.resize(2 * n);
+    s.d_forced.resize(5 * n * R);
+    s.d_nforced.resize(n);
+    s.d_dcount.resize(n);
+    s.d_dets.resize(n * dcap * 20);
+    s.d_state.resize(n * R);
+    s.d_views.resize(n * R);
+    check(zr_memcpy_async(s.d_lbox.ptr, s.h_lbox.ptr, 4 * n * 4, 0, s.stream));
+    check(zr_memcpy_async(s.d_fsize.ptr, s.h_fsize.ptr, 2 * n * 4, 0, s.stream));
+    check(zr_memcpy_async(s.d_forced.ptr, s.h_forced.ptr, 5 * n * R * 4, 0, s.stream));
+    check(zr_memcpy_async(s.d_nforced.ptr, s.h_nforced.ptr, n * 4, 0, s.stream));
+    zr_detpost_cfg pc{};
+    pc.face = is_face_detector(cfg_.detector.kind) ? 1 : 0;
+    pc.anchors = (int)A;
+    pc.params = (int)D;
+    pc.keypoints = cfg_.detector.keypoints;
+    pc.in_w = (int)dc.input_width();
+    pc.in_h = (int)dc.input_height();
+    pc.thresh = cfg_.det_threshold;
+    pc.iou = cfg_.nms_iou;
+    check(zr_detect_post_async(s.d_logits.ptr, s.d_boxes.ptr, d_anchors_.ptr, s.d_lbox.ptr, n, &pc, s.d_dcount.ptr,
+                               s.d_dets.ptr, dcap, nullptr, 0, 0, 1, s.stream));
+    const zr_track_cfg tc = track_cfg();
+    check(zr_track_seed_detections_async(s.d_dcount.ptr, s.d_dets.ptr, dcap, s.d_forced.ptr, s.d_nforced.ptr,
+                                         s.d_fsize.ptr, n, &tc, cfg_.roi_grow, cfg_.roi_use_angle ? 1 : 0,
+                                         s.d_state.ptr, s.d_views.ptr, s.stream));
+    Slot::Results &o = s.res[s.wr];
+    o.seed.resize(n * R);
+    check(zr_memcpy_async(o.seed.ptr, s.d_state.ptr, n * R * sizeof(zr_track_state), 1, s.stream));
+    const size_t nv = n * R, nout = lc.nn().num_outputs();
+    float *lptr[4] = {nullptr, nullptr, nullptr, nullptr};
+    for (size_t k = 0; k < nout && k < 4; k++) {
+        s.d_lm[k].resize((size_t)lc.nn().output_per_image(k) * nv);
+        lptr[k] = s.d_lm[k].ptr;
+    }
+    const ColorMapper cm = lc.color_mapper();
+    check(zr_cnn_estimate_device_views_async(lc.nn().handle(), s.zf.data(), n, s.d_views.ptr, nv, cm.lo, cm.hi, lptr,
+                                             s.stream));
+    const int L = cfg_.landmarker.num_landmarks;
+    s.d_lmout.resize(nv * L * 3);
+    const bool flagged = tc.kind <= 2;
+    check(zr_track_update_async(s.d_state.ptr, nv, &tc, lptr[0], (size_t)lc.nn().output_per_image(0),
+                                flagged ? lptr[1] : nullptr, flagged ? (size_t)lc.nn().output_per_image(1) : 0,
+                                s.d_lmout.ptr, s.d_views.ptr, s.stream));
+    o.dcount.resize(n);
+    o.dets.resize(n * dcap * 20);
+    o.state.resize(nv);
+    o.lmout.resize(nv * L * 3);
+    check(zr_memcpy_async(o.dcount.ptr, s.d_dcount.ptr, n * 4, 1, s.stream));
+    check(zr_memcpy_async(o.dets.ptr, s.d_dets.ptr, n * dcap * 20 * 4, 1, s.stream));
+    check(zr_memcpy_async(o.state.ptr, s.d_state.ptr, nv * sizeof(zr_track_state), 1, s.stream));
+    check(zr_memcpy_async(o.lmout.ptr, s.d_lmout.ptr, nv * L * 3 * 4, 1, s.stream));
+    for (size_t k = 2; k < nout && k < 4; k++) {  // handedness / world landmarks / tongue_out
+        const size_t cnt = (size_t)lc.nn().output_per_image(k) * nv;
+        o.extra[k - 2].resize(cnt);
+        check(zr_memcpy_async(o.extra[k - 2].ptr, lptr[k], cnt * 4, 1, s.stream));
+    }
+    check(zr_event_record(s.ev_lm, s.stream));
+    s.wr ^= 1;  // the next step of this slot writes the other set
+}
+
+void DetectTrackPipeline::finish_device(Slot &s) {
+    s.done = s.wr ^ 1;
+    const Slot::Results &o = s.res[s.done];
+    const size_t n = s.nf, R = std::max(1u, cfg_.max_rois_per_frame);
+    for (size_t i = 0; i < n; i++) {
+        times_.detections += (size_t)o.dcount[i];
+        for (size_t k = 0; k < R; k++) {
+            times_.rois += o.seed[i * R + k].active ? 1 : 0;
+            times_.tracked += o.state[i * R + k].tracked ? 1 : 0;
+        }
+    }
+    stale_ = true;
+}
+
+void DetectTrackPipeline::materialize() const {
+    if (!stale_) return;
+    stale_ = false;
+    rois_.clear();
+    for (auto &d : dets_) d.clear();
+    for (size_t k = 0; k < std::min(active_slots_, slots_.size()); k++) unpack_device(*slots_[k]);
+}
+
+// device mode, after the slot's results arrived: detections and ROI results as the host mode
+// builds them
+void DetectTrackPipeline::unpack_device(Slot &s) const {
+    const Cnn &lc = *lm_cnn_;
+    const size_t n = s.nf, R = std::max(1u, cfg_.max_rois_per_frame), dcap = cfg_.det_cap;
+    const int L = cfg_.landmarker.num_landmarks, nkp = cfg_.detector.keypoints;
+    const size_t nout = lc.nn().num_outputs();
+    const Slot::Results &o = s.res[s.done];
+    const size_t roi0 = rois_.size();
+    std::vector<uint32_t> slot_of;  // the ROI slot of each result
+    for (size_t i = 0; i < n; i++) {
+        const size_t f = s.f0 + i;
+        const int cnt = o.dcount[i];
+        auto &dets = dets_[f];
+        dets.clear();
+        for (int k = 0; k < cnt && k < (int)dcap; k++) {
+            const float *e = &o.dets[(i * dcap + k) * 20];
+            Detection d;
+            d.confidence = e[0];
+            d.angle = e[1];
+            d.rect = Rect::from_center(e[2], e[3], e[4], e[5]);
+            for (int p = 0; p < nkp; p++) d.keypoints.push_back(Vec2{e[6 + 2 * p], e[7 + 2 * p]});
+            dets.push_back(std::move(d));
+        }
+        for (size_t k = 0; k < R; k++) {
+            const zr_track_state &s0 = o.seed[i * R + k];
+            if (!s0.active) continue;
+            RoiResult r;
+            r.frame = (uint32_t)f;
+            r.from_detection = (int)k < cnt;
+            r.roi = RotatedRect(Rect::from_center(s0.roi[0], s0.roi[1], s0.roi[2], s0.roi[3]), s0.roi[4]);
+            r.result.view_rect = RotatedRect(
+                Rect::from_center(s0.view_rect[0], s0.view_rect[1], s0.view_rect[2], s0.view_rect[3]), s0.view_rect[4]);
+            rois_.push_back(std::move(r));
+            slot_of.push_back((uint32_t)(i * R + k));
+        }
+    }
+    for (size_t j = 0; j < slot_of.size(); j++) {
+        RoiResult &r = rois_[roi0 + j];
+        const size_t v = slot_of[j];
+        const zr_track_state &st = o.state[v];
+        r.confidence = st.confidence;
+        r.tracked = st.tracked != 0;
+        if (!r.tracked) continue;
+        r.result.updated_roi = RotatedRect(Rect::from_center(st.updated[0], st.updated[1], st.updated[2], st.updated[3]),
+                                           st.updated[4]);
+        r.next_roi = RotatedRect(Rect::from_center(st.roi[0], st.roi[1], st.roi[2], st.roi[3]), st.roi[4]);
+        Estimate &e = r.result.estimate;
+        const float *lm = &o.lmout[v * L * 3];
+        e.positions.assign(lm, lm + 3 * L);
+        e.confidence = st.confidence;
+        if (cfg_.landmarker.kind == NetworkKind::FaceMeshV2 && nout > 2) e.tongue_out = o.extra[0][v];
+        if (cfg_.landmarker.kind == NetworkKind::HandLandmarkLite && nout > 3) {
+            e.raw_handedness = o.extra[0][v];
+            const float *w = &o.extra[1][v * 3 * L];
+            e.world.assign(w, w + 3 * L);
+        }
+    }
 }
 
 // stage 2 (after stage 1 completed): exact decode + NMS + map (detection.rs:231-267), the
@@ -347,8 +549,21 @@ void DetectTrackPipeline::run(const std::vector<Image> &frames,
         s.nf = B / S + (k < B % S ? 1 : 0);
         f0 += s.nf;
         stage_detect(s, frames);
+        if (cfg_.device_post) stage_device_post(s, frames, forced);
     }
-    for (size_t k = 0; k < S; k++) {
+    active_slots_ = S;
+    for (size_t k = 0; k < S && cfg_.device_post; k++) {
+        Slot &s = *slots_[k];
+        const auto t = clk::now();
+        check(zr_event_synchronize(s.ev_lm));
+        times_.landmark_gpu_ms += ms_since(t);
+        finish_device(s);
+    }
+    if (cfg_.device_post) {
+        times_.total_ms = ms_since(t0);
+        return;
+    }
+    for (size_t k = 0; k < S && !cfg_.device_post; k++) {
         Slot &s = *slots_[k];
         const auto t = clk::now();
         check(zr_event_synchronize(s.ev_det));
@@ -357,7 +572,7 @@ void DetectTrackPipeline::run(const std::vector<Image> &frames,
         stage_decode_and_rois(s, frames, forced);
         times_.decode_nms_ms += ms_since(t1);
     }
-    for (size_t k = 0; k < S; k++) {
+    for (size_t k = 0; k < S && !cfg_.device_post; k++) {
         Slot &s = *slots_[k];
         const auto t = clk::now();
         if (s.nroi) check(zr_event_synchronize(s.ev_lm));
@@ -385,6 +600,7 @@ void DetectTrackPipeline::begin_steps() {
         s.nf = B / active_slots_ + (k < B % active_slots_ ? 1 : 0);
         f0 += s.nf;
         stage_detect(s, frames);
+        if (cfg_.device_post) stage_device_post(s, frames, forced_);
     }
 }
 
@@ -394,7 +610,27 @@ void DetectTrackPipeline::step(bool more) {
     if (S == 0) return;
     dets_.assign(B, {});
     rois_.clear();
-    for (size_t k = 0; k < S; k++) {
+    // device mode: a slot's whole step is on its stream; take its results and enqueue its next
+    // step at once, while the other slots' steps run
+    for (size_t k = 0; k < S && cfg_.device_post; k++) {
+        Slot &s = *slots_[k];
+        const auto t = clk::now();
+        check(zr_event_synchronize(s.ev_lm));
+        times_.landmark_gpu_ms += ms_since(t);
+        const auto t1 = clk::now();
+        finish_device(s);
+        if (more) {
+            stage_detect(s, frames);
+            stage_device_post(s, frames, forced_);
+        }
+        times_.map_ms += ms_since(t1);
+    }
+    if (cfg_.device_post) {
+        times_.frames += B;
+        times_.total_ms = ms_since(steps_t0_);
+        return;
+    }
+    for (size_t k = 0; k < S && !cfg_.device_post; k++) {
         Slot &s = *slots_[k];
         const auto t = clk::now();
         check(zr_event_synchronize(s.ev_det));
@@ -407,7 +643,7 @@ void DetectTrackPipeline::step(bool more) {
         // letterbox views are consumed; the landmark launch copied its view descriptors)
         if (more) stage_detect(s, frames);
     }
-    for (size_t k = 0; k < S; k++) {
+    for (size_t k = 0; k < S && !cfg_.device_post; k++) {
         Slot &s = *slots_[k];
         const auto t = clk::now();
         if (s.nroi) check(zr_event_synchronize(s.ev_lm));

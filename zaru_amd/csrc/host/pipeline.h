@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "detection.h"
+#include "device_tracker.h"
 #include "landmark.h"
 
 namespace zh {
@@ -70,6 +71,14 @@ struct PipelineConfig {
     // give each sub-batch its own HIP stream (kernels of different sub-batches may then run
     // concurrently on the GPU); false = one stream, kernels strictly back to back
     bool stream_per_sub_batch = true;
+    // decode + NMS + map, the ROI seeding and the tracker update on the device
+    // (zr_detect_post_async -> zr_track_seed_detections_async -> landmarks ->
+    // zr_track_update_async, one stream per sub-batch, no host step in between); false = the
+    // host restatement (decode/NMS/map and the tracker update on the thread pool).  Both give
+    // the same bits; device mode keeps the first det_cap detections of a frame (the count stays
+    // exact).
+    bool device_post = true;
+    uint32_t det_cap = 16;
     static PipelineConfig face();  // BlazeFace -> FaceMesh V1 (config 3)
     static PipelineConfig hand();  // BlazePalm lite -> hand landmark lite (config 4)
 };
@@ -83,8 +92,14 @@ class DetectTrackPipeline {
     // detection (may be empty).  Synchronous; results valid until the next run.
     void run(const std::vector<Image> &frames, const std::vector<std::vector<RotatedRect>> &forced);
 
-    const std::vector<std::vector<Detection>> &detections() const { return dets_; }
-    const std::vector<RoiResult> &rois() const { return rois_; }
+    const std::vector<std::vector<Detection>> &detections() const {
+        materialize();
+        return dets_;
+    }
+    const std::vector<RoiResult> &rois() const {
+        materialize();
+        return rois_;
+    }
     const StageTimes &times() const { return times_; }
     const PipelineConfig &config() const { return cfg_; }
     double detector_bytes_per_image() const;
@@ -128,7 +143,31 @@ class DetectTrackPipeline {
         std::vector<zr_view> rv;
         std::vector<uint32_t> rf;
         size_t roi0 = 0, nroi = 0;
+        // device post-processing (PipelineConfig::device_post)
+        DeviceArray<float> d_lbox, d_forced, d_dets, d_lmout;
+        DeviceArray<uint32_t> d_fsize;
+        DeviceArray<int32_t> d_nforced, d_dcount;
+        DeviceArray<zr_track_state> d_state;
+        DeviceArray<zr_view_desc> d_views;
+        PinnedArray<float> h_lbox, h_forced;
+        PinnedArray<uint32_t> h_fsize;
+        PinnedArray<int32_t> h_nforced;
+        // a step's results arrive in one of two host sets: the one a finished step filled is
+        // read (lazily, materialize()) while the next step's copies land in the other
+        struct Results {
+            PinnedArray<int32_t> dcount;
+            PinnedArray<float> dets, lmout, extra[2];
+            PinnedArray<zr_track_state> seed, state;
+        } res[2];
+        int wr = 0;    // the set the enqueued step writes
+        int done = 0;  // the set of the last finished step
     };
+    void stage_device_post(Slot &s, const std::vector<Image> &frames,
+                           const std::vector<std::vector<RotatedRect>> &forced);
+    void finish_device(Slot &s);  // the slot's step completed: counts; results readable
+    void unpack_device(Slot &s) const;
+    void materialize() const;
+    zr_track_cfg track_cfg() const;
     void stage_detect(Slot &s, const std::vector<Image> &frames);
     void stage_decode_and_rois(Slot &s, const std::vector<Image> &frames,
                                const std::vector<std::vector<RotatedRect>> &forced);
@@ -137,12 +176,14 @@ class DetectTrackPipeline {
     PipelineConfig cfg_;
     int device_;
     std::shared_ptr<const Cnn> det_cnn_, lm_cnn_;
+    DeviceArray<float> d_anchors_;  // [A][2], device post-processing
     NonMaxSuppression nms_;
     ThreadPool pool_;
     void *stream_ = nullptr;
     std::vector<std::unique_ptr<Slot>> slots_;
-    std::vector<std::vector<Detection>> dets_;
-    std::vector<RoiResult> rois_;
+    mutable std::vector<std::vector<Detection>> dets_;
+    mutable std::vector<RoiResult> rois_;
+    mutable bool stale_ = false;  // device mode: dets_ / rois_ not yet built from the last step
     StageTimes times_;
     std::vector<Image> frames_;
     std::vector<std::vector<RotatedRect>> forced_;

@@ -887,8 +887,8 @@ template <int K, int S, int WM, int MTW, int DFKC>
 static size_t dma_plan(const DwPwParams &p, int *runmax, int *bufsz) {
     constexpr int BN = (4 / WM) * 32, BM = WM * MTW * 32, KKP = (DFKC * K * K + 3) / 4 * 4;
     const int H = p.in.H, W = p.in.W, Pin = H * W, Pq = p.g.P, OW = p.OW;
-    const int nimg = p.g.ncols / Pq;
-    if (!form_on(FORM_DMA) || p.in.sN != Pin || p.in.sC % 4 || ((int64_t)nimg * Pin) % 4 || p.g.K % 4 ||
+    // (runs are rounded out to 16-B ends inside the channel plane: sC % 4 == 0 leaves room)
+    if (!form_on(FORM_DMA) || p.in.sN != Pin || p.in.sC % 4 || p.g.K % 4 ||
         ((uintptr_t)p.in.p | (uintptr_t)p.g.wt | (uintptr_t)p.dw_w | (uintptr_t)p.dw_b) % 16)
         return 0;
     int rm = 0;

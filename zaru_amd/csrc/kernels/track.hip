@@ -13,60 +13,12 @@
 // glibc's own sinf / cosf / atan2f / expf (glibc_math.h, verified over every f32 input), so the
 // update and the view table it writes are bit-identical to the host restatement.
 #include "../runtime/zr_track.h"
-#include "glibc_math.h"
+#include "geom_dev.h"
 
 namespace zr {
 namespace {
 
-struct V2 {
-    float x, y;
-};
-struct RRect {  // Rect as (centre, size) (rect.rs:15-18) + rotation
-    float cx, cy, w, h, rad;
-};
-
-__device__ __forceinline__ V2 rot_ccw(V2 v, float r) {  // matrix.rs:571-579, ops.rs:68-77
-    const float c = glibc::cosf(r), s = glibc::sinf(r), ns = -s;
-    return {(0.f + c * v.x) + ns * v.y, (0.f + s * v.x) + c * v.y};
-}
-
-__device__ __forceinline__ float signed_angle_to(V2 a, V2 b) {  // vector.rs:568-573
-    const float perp = a.x * b.y - a.y * b.x;
-    const float dot = (0.f + a.x * b.x) + a.y * b.y;
-    return -glibc::atan2f(perp, dot);
-}
-
-__device__ __forceinline__ RRect from_top_left(float x, float y, float w, float h, float rad) {
-    return {x + w * 0.5f, y + h * 0.5f, w, h, rad};
-}
-
-__device__ __forceinline__ V2 top_left(const RRect &r) { return {r.cx - r.w * 0.5f, r.cy - r.h * 0.5f}; }
-
-__device__ __forceinline__ RRect grow_to_fit_aspect(RRect r, int aw, int ah) {  // rect.rs:104-117
-    const float a = (float)aw / (float)ah;
-    const float tw = r.h * a;
-    if (tw >= r.w) {
-        r.w += tw - r.w;
-    } else {
-        const float th = r.w / a;
-        r.h += th - r.h;
-    }
-    return r;
-}
-
-__device__ __forceinline__ V2 transform_out(const RRect &r, V2 p) {  // rect.rs:417-423
-    const V2 half = {r.w * 0.5f, r.h * 0.5f};
-    const V2 q = rot_ccw({p.x - half.x, p.y - half.y}, r.rad);
-    const V2 tl = top_left(r);
-    return {q.x + half.x + tl.x, q.y + half.y + tl.y};
-}
-
-// ViewData::view (image/mod.rs:201-210): child in the parent's local coordinates
-__device__ __forceinline__ RRect view_of(const RRect &parent, const RRect &child) {
-    const float rad = parent.rad + child.rad;
-    const V2 c = transform_out(parent, {child.cx, child.cy});
-    return from_top_left(c.x - child.w * 0.5f, c.y - child.h * 0.5f, child.w, child.h, rad);
-}
+using namespace geo;
 
 // The next estimate's sampling view of a RoI: track_impl's view_rect + Estimator's aspect-fit
 // local rect (pipeline.cpp stage_decode_and_rois, landmark.rs:465-467 + 320-323).
@@ -128,7 +80,7 @@ __global__ __launch_bounds__(256) void track_kernel(const TrackParams P) {
             return;
         }
         float conf = 1.f;
-        if (P.kind == 0) conf = 1.f / (1.f + glibc::expf(-P.flag[(int64_t)i * P.flag_stride]));  // num.rs:6-8
+        if (P.kind == 0) conf = sigmoid(P.flag[(int64_t)i * P.flag_stride]);  // num.rs:6-8
         else if (P.kind == 1) conf = P.flag[(int64_t)i * P.flag_stride];
         if (conf < P.loss_thresh) {
             invalidate_rows(P, i, tid);
@@ -235,7 +187,41 @@ __global__ __launch_bounds__(256) void track_kernel(const TrackParams P) {
     } else if (tid != 0) {
         return;
     }
-    next_view(st, P.views[i], i, P.asp_w, P.asp_h);
+    next_view(st, P.views[i], i / P.rpf, P.asp_w, P.asp_h);
+    P.state[i] = st;
+}
+
+// One thread per ROI slot (frame f = i / R, slot k = i % R): the seed ROI the host pipeline
+// builds (pipeline.cpp stage_decode_and_rois: RotatedRect(det.rect[.grow_rel(g)], angle or 0)
+// per detection in NMS order, up to R, or the frame's forced ROIs when it has no detection) and
+// its first view, as LandmarkTracker::set_roi + track_impl would sample it.
+__global__ __launch_bounds__(256) void seed_kernel(const SeedParams P) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= P.N * P.R) return;
+    const int f = i / P.R, k = i - f * P.R;
+    const int cnt = P.count[f];
+    TrackState st{};
+    st.frame_w = P.fsize[2 * f];
+    st.frame_h = P.fsize[2 * f + 1];
+    if (k < cnt && k < P.dcap) {
+        const float *d = P.dets + ((int64_t)f * P.dcap + k) * 20;
+        RRect r = {d[2], d[3], d[4], d[5], P.roi_use_angle ? d[1] : 0.f};
+        if (P.roi_grow > 0.f) r = grow_rel(r, P.roi_grow);
+        st.roi[0] = r.cx;
+        st.roi[1] = r.cy;
+        st.roi[2] = r.w;
+        st.roi[3] = r.h;
+        st.roi[4] = r.rad;
+        st.active = 1;
+    } else if (cnt == 0 && P.nforced && k < P.nforced[f]) {
+        const float *r = P.forced + ((int64_t)f * P.R + k) * 5;
+        for (int c = 0; c < 5; ++c) st.roi[c] = r[c];
+        st.active = 1;
+    } else {  // idle slot: a valid (empty-frame) view so the batched network stays in bounds
+        st.roi[2] = st.roi[3] = 1.f;
+        st.active = 0;
+    }
+    next_view(st, P.views[i], f, P.asp_w, P.asp_h);
     P.state[i] = st;
 }
 
@@ -244,6 +230,11 @@ __global__ __launch_bounds__(256) void track_kernel(const TrackParams P) {
 const char *launch_track(const TrackParams &p, hipStream_t s) {
     hipLaunchKernelGGL(track_kernel, dim3(p.n), dim3(256), 0, s, p);
     return "track_kernel";
+}
+
+const char *launch_seed(const SeedParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(seed_kernel, dim3((p.N * p.R + 255) / 256), dim3(256), 0, s, p);
+    return "seed_kernel";
 }
 
 // Test hook (zr_debug_glibc_math): the device evaluation of glibc_math.h, one thread per input.

@@ -1292,9 +1292,9 @@ Resolved resolve(const TRef &r, const Plan &plan, const Binding &b) {
     Resolved o{};
     const int64_t P = (int64_t)r.H * r.W;
     if (r.kind == 0) {
-        o.p = b.arena + plan.storage_off[r.id] * b.N + (int64_t)r.c_off * P * b.N;
+        o.p = b.arena + plan.storage_off[r.id] * b.Ns + (int64_t)r.c_off * P * b.Ns;
         o.sN = P;
-        o.sC = P * b.N;
+        o.sC = P * b.Ns;
         o.sP = 1;
     } else if (r.kind == 1) {
         o.p = b.input;

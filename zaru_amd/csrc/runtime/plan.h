@@ -89,6 +89,10 @@ bool compile_plan(const OnnxModel &m, const std::vector<uint32_t> &out_sel, Plan
 
 struct Binding {
     int N = 0;
+    // the batch the arena is laid out for: N rounded up to a multiple of 4, so every internal
+    // channel plane (P * Ns floats) starts 16-B aligned whatever N and P are -- the LDS-DMA forms
+    // need that (the padding images are never computed or read as results)
+    int Ns = 0;
     const float *input = nullptr;
     int64_t in_sN = 0, in_sC = 0;   // input strides (NCHW user tensor or CNHW preproc output)
     float *const *outputs = nullptr;  // device pointers, one per plan output

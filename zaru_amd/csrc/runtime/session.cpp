@@ -234,7 +234,8 @@ struct CtxLock {
 // enqueue the plan on `stream` with a context's workspace
 int enqueue(zr_session *s, Ctx *c, int N, const float *input, int64_t in_sN, int64_t in_sC,
             float *const *outs, hipStream_t stream, const zr::PreprocParams *pre = nullptr) {
-    const size_t need = (size_t)s->plan.arena_per_image * (size_t)N;
+    const int Ns = (N + 3) / 4 * 4;  // zr::Binding::Ns
+    const size_t need = (size_t)s->plan.arena_per_image * (size_t)Ns;
     // kernels address every tensor with 32-bit element offsets (kernels/epilogue.h)
     size_t largest = std::max(need, (size_t)(input ? in_sN : 0) * (size_t)N);
     for (const auto &o : s->plan.outputs) largest = std::max(largest, (size_t)o.per_image * (size_t)N);
@@ -244,6 +245,7 @@ int enqueue(zr_session *s, Ctx *c, int N, const float *input, int64_t in_sN, int
     HIP_TRY(hipStreamWaitEvent(stream, c->done, 0));
     zr::Binding b;
     b.N = N;
+    b.Ns = Ns;
     b.input = input;
     b.in_sN = in_sN;
     b.in_sC = in_sC;
@@ -609,6 +611,8 @@ static int track_params(zr::TrackParams &p, zr_track_state *d_state, size_t n, c
     p.asp_h = cfg->aspect_h;
     p.loss_thresh = cfg->loss_thresh;
     p.padding = cfg->padding;
+    if (cfg->rois_per_frame < 0) return set_err(ZR_ERR_INVALID_ARGUMENT, "rois_per_frame must be >= 0");
+    p.rpf = cfg->rois_per_frame > 0 ? cfg->rois_per_frame : 1;
     return ZR_OK;
 }
 
@@ -646,6 +650,79 @@ int zr_track_update_async(zr_track_state *d_state, size_t n, const zr_track_cfg 
         p.flag_stride = (int)flag_stride;
         p.lm_out = d_lm_out;
         zr::launch_track(p, (hipStream_t)hip_stream);
+        HIP_TRY(hipGetLastError());
+        return ZR_OK;
+    });
+}
+
+int zr_detect_post_async(const float *d_logits, const float *d_boxes, const float *d_anchors,
+                         const float *d_letterbox, size_t n, const zr_detpost_cfg *cfg, int32_t *d_count,
+                         float *d_dets, size_t dcap, float *d_records, size_t rmax, uint32_t first_id,
+                         uint32_t id_stride, void *hip_stream) {
+    return guarded([&]() -> int {
+        if (!d_logits || !d_boxes || !d_anchors || !d_letterbox || !cfg || !d_count || (!d_dets && dcap))
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument");
+        if (n == 0) return ZR_OK;
+        if (cfg->anchors <= 0 || cfg->keypoints < 3 || cfg->keypoints > 7 ||
+            cfg->params < 4 + 2 * cfg->keypoints || cfg->in_w <= 0 || cfg->in_h <= 0 || n > (1u << 24) ||
+            dcap > 4096 || rmax > 64 || (d_records && rmax == 0))
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "bad detection post-processing configuration");
+        zr::DetPostParams p{};
+        p.logits = d_logits;
+        p.boxes = d_boxes;
+        p.anchors = d_anchors;
+        p.letterbox = d_letterbox;
+        p.N = (int)n;
+        p.A = cfg->anchors;
+        p.D = cfg->params;
+        p.nkp = cfg->keypoints;
+        p.face = cfg->face ? 1 : 0;
+        p.in_w = cfg->in_w;
+        p.in_h = cfg->in_h;
+        p.thresh = cfg->thresh;
+        p.iou = cfg->iou;
+        p.count = d_count;
+        p.dets = d_dets;
+        p.dcap = (int)dcap;
+        p.rec = d_records;
+        p.rmax = (int)rmax;
+        p.first_id = first_id;
+        p.id_stride = id_stride;
+        if (zr::det_post_lds(p.A) > 128 * 1024) return set_err(ZR_ERR_INVALID_ARGUMENT, "too many anchors");
+        zr::launch_det_post(p, (hipStream_t)hip_stream);
+        HIP_TRY(hipGetLastError());
+        return ZR_OK;
+    });
+}
+
+int zr_track_seed_detections_async(const int32_t *d_count, const float *d_dets, size_t dcap, const float *d_forced,
+                                   const int32_t *d_nforced, const uint32_t *d_frame_size, size_t n,
+                                   const zr_track_cfg *cfg, float roi_grow, int roi_use_angle,
+                                   zr_track_state *d_state, zr_view_desc *d_views, void *hip_stream) {
+    return guarded([&]() -> int {
+        if (!d_count || !d_dets || !d_frame_size || !cfg || !d_state || !d_views || dcap == 0 ||
+            (!d_forced != !d_nforced))
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument");
+        if (n == 0) return ZR_OK;
+        const int R = cfg->rois_per_frame > 0 ? cfg->rois_per_frame : 1;
+        if (cfg->aspect_w <= 0 || cfg->aspect_h <= 0 || R > 64 || (uint64_t)n * R > (1u << 24) || !(roi_grow >= 0.f))
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "bad tracker seeding configuration");
+        zr::SeedParams p{};
+        p.count = d_count;
+        p.dets = d_dets;
+        p.dcap = (int)dcap;
+        p.forced = d_forced;
+        p.nforced = d_nforced;
+        p.fsize = d_frame_size;
+        p.N = (int)n;
+        p.R = R;
+        p.roi_grow = roi_grow;
+        p.roi_use_angle = roi_use_angle ? 1 : 0;
+        p.asp_w = cfg->aspect_w;
+        p.asp_h = cfg->aspect_h;
+        p.state = reinterpret_cast<zr::TrackState *>(d_state);
+        p.views = reinterpret_cast<zr::ViewDesc *>(d_views);
+        zr::launch_seed(p, (hipStream_t)hip_stream);
         HIP_TRY(hipGetLastError());
         return ZR_OK;
     });

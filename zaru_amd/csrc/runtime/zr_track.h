@@ -36,9 +36,48 @@ struct TrackParams {
     int asp_w, asp_h;      // network aspect ratio, reduced
     float loss_thresh, padding;
     int seed;              // 1: only derive views from state.roi (no estimate to consume)
+    int rpf;               // ROIs per frame: ROI i samples frame i / rpf
 };
 
 const char *launch_track(const TrackParams &p, hipStream_t s);
+
+// Detector::detect_impl after inference (detpost.hip): extract, weighted NMS, map to frame px.
+struct DetPostParams {
+    const float *logits;    // [N][A] raw classificator logits
+    const float *boxes;     // [N][A][D] raw regressors
+    const float *anchors;   // [A][2] anchor centres (ssd.rs:96-119)
+    const float *letterbox; // [N][4] the letterbox Rect (cx, cy, w, h) each frame was sampled with
+    int N, A, D, nkp;       // frames, anchors, params per anchor, keypoints
+    int face;               // 1: angle = eye line vs +X (BlazeFace); 0: wrist -> MCP vs +Y (palm)
+    int in_w, in_h;         // detector input
+    float thresh, iou;
+    int *count;             // [N] detections after NMS
+    float *dets;            // [N][dcap][20] {conf, angle, cx, cy, w, h, 7 x (kx, ky)}, NMS order
+    int dcap;
+    float *rec;             // [N][2 + 20 rmax] all-gather records (may be null)
+    int rmax;
+    uint32_t first_id, id_stride;
+};
+const char *launch_det_post(const DetPostParams &p, hipStream_t s);
+size_t det_post_lds(int anchors);
+
+// Tracker seeding from detections (track.hip): ROI slot k < R of frame f is detection k
+// (grow_rel + angle as configured), else -- when the frame has none -- forced ROI k, else idle.
+struct SeedParams {
+    const int *count;        // [N] (det_post)
+    const float *dets;       // [N][dcap][20]
+    int dcap;
+    const float *forced;     // [N][R][5] (cx, cy, w, h, rad); may be null
+    const int *nforced;      // [N]; may be null
+    const uint32_t *fsize;   // [N][2] frame width, height
+    int N, R;
+    float roi_grow;
+    int roi_use_angle;
+    int asp_w, asp_h;
+    TrackState *state;       // [N * R] out
+    ViewDesc *views;         // [N * R] out
+};
+const char *launch_seed(const SeedParams &p, hipStream_t s);
 // fn: 0 sinf, 1 cosf, 2 expf, 3 atanf, 4 atan2f(a, b) -- glibc_math.h on the device
 const char *launch_glibc_math(int fn, const float *a, const float *b, float *out, int64_t n, hipStream_t s);
 
