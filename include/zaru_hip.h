@@ -183,12 +183,13 @@ int zr_view_describe(const zr_view *views, size_t n, uint32_t frame, zr_view_des
  * R = cfg->rois_per_frame) is RotatedRect(det_k.rect[.grow_rel(roi_grow)], roi_use_angle ?
  * det_k.angle : 0) for the frame's first R detections (NMS order), else -- when the frame has no
  * detection -- its forced ROI k (d_forced [n][R][5], d_nforced [n]; both may be NULL), else the
- * slot is idle (active = 0).  Writes the states and their first views (frame f). */
+ * slot is idle (active = 0).  Writes the states, optionally a copy of them (d_seed_copy, may be
+ * NULL: the update rewrites the states), and their first views (frame f). */
 int zr_track_seed_detections_async(const int32_t *d_count, const float *d_dets, size_t dcap,
                                    const float *d_forced, const int32_t *d_nforced,
                                    const uint32_t *d_frame_size, size_t n, const zr_track_cfg *cfg,
                                    float roi_grow, int roi_use_angle, zr_track_state *d_state,
-                                   zr_view_desc *d_views, void *hip_stream);
+                                   zr_track_state *d_seed_copy, zr_view_desc *d_views, void *hip_stream);
 /* Cnn::estimate (nn/mod.rs:118-126) with a device-resident view table (frames: host array). */
 int zr_cnn_estimate_device_views_async(zr_session *s, const zr_frame *frames, size_t n_frames,
                                        const zr_view_desc *d_views, size_t n_views, float lo,

@@ -174,6 +174,7 @@ std::string DetectTrackPipeline::profile_read() {
 void DetectTrackPipeline::set_frames(std::vector<Image> frames, std::vector<std::vector<RotatedRect>> forced) {
     frames_ = std::move(frames);
     forced_ = std::move(forced);
+    for (auto &s : slots_) s->inputs_ok = false;
 }
 
 namespace {
@@ -234,51 +235,62 @@ zr_track_cfg DetectTrackPipeline::track_cfg() const {
 
 // device mode, enqueued right behind stage 1 on the slot's stream: decode + NMS + map
 // (zr_detect_post_async), the ROI seeds and their views (zr_track_seed_detections_async), the
-// landmark network on those views and the tracker update (zr_track_update_async), then the
-// results' copies to the host.  ROI slot k of frame f is detection k (NMS order) or, when the
-// frame has none, forced ROI k -- the host mode's seeds -- else idle.
+// landmark network on those views and the tracker update (zr_track_update_async), then one copy
+// of the step's summary to the host.  ROI slot k of frame f is detection k (NMS order) or, when
+// the frame has none, forced ROI k -- the host mode's seeds -- else idle.
 void DetectTrackPipeline::stage_device_post(Slot &s, const std::vector<Image> &frames,
                                             const std::vector<std::vector<RotatedRect>> &forced) {
     const Cnn &dc = *det_cnn_, &lc = *lm_cnn_;
     const size_t n = s.nf, R = std::max(1u, cfg_.max_rois_per_frame), dcap = cfg_.det_cap;
+    const size_t nv = n * R, nout = lc.nn().num_outputs();
+    const int L = cfg_.landmarker.num_landmarks;
     const uint32_t A = (uint32_t)cfg_.detector.anchors().size(), D = (uint32_t)cfg_.detector.params;
-    s.h_lbox.resize(4 * n);
-    s.h_fsize.resize(2 * n);
-    s.h_forced.resize(5 * n * R);
-    s.h_nforced.resize(n);
-    for (size_t i = 0; i < n; i++) {
-        const size_t f = s.f0 + i;
-        const Rect &r = s.letterbox[i];
-        s.h_lbox[4 * i] = r.center().x;
-        s.h_lbox[4 * i + 1] = r.center().y;
-        s.h_lbox[4 * i + 2] = r.width();
-        s.h_lbox[4 * i + 3] = r.height();
-        s.h_fsize[2 * i] = frames[f].width;
-        s.h_fsize[2 * i + 1] = frames[f].height;
-        const size_t nf = f < forced.size() ? std::min(R, forced[f].size()) : 0;
-        s.h_nforced[i] = (int32_t)nf;
-        for (size_t k = 0; k < nf; k++) {
-            const RotatedRect &q = forced[f][k];
-            float *o = &s.h_forced[5 * (i * R + k)];
-            o[0] = q.rect().center().x;
-            o[1] = q.rect().center().y;
-            o[2] = q.rect().width();
-            o[3] = q.rect().height();
-            o[4] = q.rotation_radians();
+    if (!s.inputs_ok) {  // letterbox rects, frame sizes, forced ROIs: fixed for a frame set
+        s.h_lbox.resize(4 * n);
+        s.h_fsize.resize(2 * n);
+        s.h_forced.resize(5 * nv);
+        s.h_nforced.resize(n);
+        for (size_t i = 0; i < n; i++) {
+            const size_t f = s.f0 + i;
+            const Rect &r = s.letterbox[i];
+            s.h_lbox[4 * i] = r.center().x;
+            s.h_lbox[4 * i + 1] = r.center().y;
+            s.h_lbox[4 * i + 2] = r.width();
+            s.h_lbox[4 * i + 3] = r.height();
+            s.h_fsize[2 * i] = frames[f].width;
+            s.h_fsize[2 * i + 1] = frames[f].height;
+            const size_t nf = f < forced.size() ? std::min(R, forced[f].size()) : 0;
+            s.h_nforced[i] = (int32_t)nf;
+            for (size_t k = 0; k < nf; k++) {
+                const RotatedRect &q = forced[f][k];
+                float *o = &s.h_forced[5 * (i * R + k)];
+                o[0] = q.rect().center().x;
+                o[1] = q.rect().center().y;
+                o[2] = q.rect().width();
+                o[3] = q.rect().height();
+                o[4] = q.rotation_radians();
+            }
         }
+        s.d_lbox.resize(4 * n);
+        s.d_fsize.resize(2 * n);
+        s.d_forced.resize(5 * nv);
+        s.d_nforced.resize(n);
+        check(zr_memcpy_async(s.d_lbox.ptr, s.h_lbox.ptr, 4 * n * 4, 0, s.stream));
+        check(zr_memcpy_async(s.d_fsize.ptr, s.h_fsize.ptr, 2 * n * 4, 0, s.stream));
+        check(zr_memcpy_async(s.d_forced.ptr, s.h_forced.ptr, 5 * nv * 4, 0, s.stream));
+        check(zr_memcpy_async(s.d_nforced.ptr, s.h_nforced.ptr, n * 4, 0, s.stream));
+        s.inputs_ok = true;
     }
-    s.d_lbox.resize(4 * n);
-    s.d_fsize.resize(2 * n);
-    s.d_forced.resize(5 * n * R);
-    s.d_nforced.resize(n);
-    s.d_dcount.resize(n);
-    s.d_dets.resize(n * dcap * 20);
-    s.d_state.resize(n * R);
-    s.d_views.resize(n * R);
-    check(zr_memcpy_async(s.d_lbox.ptr, s.h_lbox.ptr, 4 * n * 4, 0, s.stream));
-    check(zr_memcpy_async(s.d_fsize.ptr, s.h_fsize.ptr, 2 * n * 4, 0, s.stream));
-    check(zr_memcpy_async(s.d_forced.ptr, s.h_forced.ptr, 5 * n * R * 4, 0, s.stream));
-    check(zr_memcpy_async(s.d_nforced.ptr, s.h_nforced.ptr, n * 4, 0, s.stream));
+    Slot::Results &o = s.res[s.wr];
+    const size_t sum_bytes = 2 * nv * sizeof(zr_track_state) + n * sizeof(int32_t);
+    o.sum.resize(sum_bytes);
+    o.h_sum.resize(sum_bytes);
+    o.dets.resize(n * dcap * 20);
+    o.lmout.resize(nv * L * 3);
+    zr_track_state *d_state = reinterpret_cast<zr_track_state *>(o.sum.ptr);
+    zr_track_state *d_seed = d_state + nv;
+    int32_t *d_count = reinterpret_cast<int32_t *>(d_seed + nv);
+    s.d_views.resize(nv);
     zr_detpost_cfg pc{};
     pc.face = is_face_detector(cfg_.detector.kind) ? 1 : 0;
     pc.anchors = (int)A;
@@ -288,43 +300,25 @@ void DetectTrackPipeline::stage_device_post(Slot &s, const std::vector<Image> &f
     pc.in_h = (int)dc.input_height();
     pc.thresh = cfg_.det_threshold;
     pc.iou = cfg_.nms_iou;
-    check(zr_detect_post_async(s.d_logits.ptr, s.d_boxes.ptr, d_anchors_.ptr, s.d_lbox.ptr, n, &pc, s.d_dcount.ptr,
-                               s.d_dets.ptr, dcap, nullptr, 0, 0, 1, s.stream));
+    check(zr_detect_post_async(s.d_logits.ptr, s.d_boxes.ptr, d_anchors_.ptr, s.d_lbox.ptr, n, &pc, d_count,
+                               o.dets.ptr, dcap, nullptr, 0, 0, 1, s.stream));
     const zr_track_cfg tc = track_cfg();
-    check(zr_track_seed_detections_async(s.d_dcount.ptr, s.d_dets.ptr, dcap, s.d_forced.ptr, s.d_nforced.ptr,
-                                         s.d_fsize.ptr, n, &tc, cfg_.roi_grow, cfg_.roi_use_angle ? 1 : 0,
-                                         s.d_state.ptr, s.d_views.ptr, s.stream));
-    Slot::Results &o = s.res[s.wr];
-    o.seed.resize(n * R);
-    check(zr_memcpy_async(o.seed.ptr, s.d_state.ptr, n * R * sizeof(zr_track_state), 1, s.stream));
-    const size_t nv = n * R, nout = lc.nn().num_outputs();
+    check(zr_track_seed_detections_async(d_count, o.dets.ptr, dcap, s.d_forced.ptr, s.d_nforced.ptr, s.d_fsize.ptr,
+                                         n, &tc, cfg_.roi_grow, cfg_.roi_use_angle ? 1 : 0, d_state, d_seed,
+                                         s.d_views.ptr, s.stream));
     float *lptr[4] = {nullptr, nullptr, nullptr, nullptr};
     for (size_t k = 0; k < nout && k < 4; k++) {
-        s.d_lm[k].resize((size_t)lc.nn().output_per_image(k) * nv);
-        lptr[k] = s.d_lm[k].ptr;
+        o.lm[k].resize((size_t)lc.nn().output_per_image(k) * nv);
+        lptr[k] = o.lm[k].ptr;
     }
     const ColorMapper cm = lc.color_mapper();
     check(zr_cnn_estimate_device_views_async(lc.nn().handle(), s.zf.data(), n, s.d_views.ptr, nv, cm.lo, cm.hi, lptr,
                                              s.stream));
-    const int L = cfg_.landmarker.num_landmarks;
-    s.d_lmout.resize(nv * L * 3);
     const bool flagged = tc.kind <= 2;
-    check(zr_track_update_async(s.d_state.ptr, nv, &tc, lptr[0], (size_t)lc.nn().output_per_image(0),
+    check(zr_track_update_async(d_state, nv, &tc, lptr[0], (size_t)lc.nn().output_per_image(0),
                                 flagged ? lptr[1] : nullptr, flagged ? (size_t)lc.nn().output_per_image(1) : 0,
-                                s.d_lmout.ptr, s.d_views.ptr, s.stream));
-    o.dcount.resize(n);
-    o.dets.resize(n * dcap * 20);
-    o.state.resize(nv);
-    o.lmout.resize(nv * L * 3);
-    check(zr_memcpy_async(o.dcount.ptr, s.d_dcount.ptr, n * 4, 1, s.stream));
-    check(zr_memcpy_async(o.dets.ptr, s.d_dets.ptr, n * dcap * 20 * 4, 1, s.stream));
-    check(zr_memcpy_async(o.state.ptr, s.d_state.ptr, nv * sizeof(zr_track_state), 1, s.stream));
-    check(zr_memcpy_async(o.lmout.ptr, s.d_lmout.ptr, nv * L * 3 * 4, 1, s.stream));
-    for (size_t k = 2; k < nout && k < 4; k++) {  // handedness / world landmarks / tongue_out
-        const size_t cnt = (size_t)lc.nn().output_per_image(k) * nv;
-        o.extra[k - 2].resize(cnt);
-        check(zr_memcpy_async(o.extra[k - 2].ptr, lptr[k], cnt * 4, 1, s.stream));
-    }
+                                o.lmout.ptr, s.d_views.ptr, s.stream));
+    check(zr_memcpy_async(o.h_sum.ptr, o.sum.ptr, sum_bytes, 1, s.stream));
     check(zr_event_record(s.ev_lm, s.stream));
     s.wr ^= 1;  // the next step of this slot writes the other set
 }
@@ -332,13 +326,13 @@ void DetectTrackPipeline::stage_device_post(Slot &s, const std::vector<Image> &f
 void DetectTrackPipeline::finish_device(Slot &s) {
     s.done = s.wr ^ 1;
     const Slot::Results &o = s.res[s.done];
-    const size_t n = s.nf, R = std::max(1u, cfg_.max_rois_per_frame);
-    for (size_t i = 0; i < n; i++) {
-        times_.detections += (size_t)o.dcount[i];
-        for (size_t k = 0; k < R; k++) {
-            times_.rois += o.seed[i * R + k].active ? 1 : 0;
-            times_.tracked += o.state[i * R + k].tracked ? 1 : 0;
-        }
+    const size_t n = s.nf, R = std::max(1u, cfg_.max_rois_per_frame), nv = n * R;
+    const zr_track_state *st = reinterpret_cast<const zr_track_state *>(o.h_sum.ptr);
+    const int32_t *cnt = reinterpret_cast<const int32_t *>(st + 2 * nv);
+    for (size_t i = 0; i < n; i++) times_.detections += (size_t)cnt[i];
+    for (size_t v = 0; v < nv; v++) {
+        times_.rois += st[nv + v].active ? 1 : 0;
+        times_.tracked += st[v].tracked ? 1 : 0;
     }
     stale_ = true;
 }
@@ -351,32 +345,45 @@ void DetectTrackPipeline::materialize() const {
     for (size_t k = 0; k < std::min(active_slots_, slots_.size()); k++) unpack_device(*slots_[k]);
 }
 
-// device mode, after the slot's results arrived: detections and ROI results as the host mode
-// builds them
+// device mode, on demand: the last finished step's detections and ROI results as the host mode
+// builds them (the set stays untouched until the slot's next step after this one is enqueued).
+// The copies go on the null stream: the set is complete (its ev_lm was waited for), and one more
+// stream would share a hardware queue with a slot's (GPU_MAX_HW_QUEUES = 4: null + 3 slots) and
+// serialise two slots -- measured 12% slower on the face line (profiles/, r03i trace)
 void DetectTrackPipeline::unpack_device(Slot &s) const {
     const Cnn &lc = *lm_cnn_;
-    const size_t n = s.nf, R = std::max(1u, cfg_.max_rois_per_frame), dcap = cfg_.det_cap;
+    const size_t n = s.nf, R = std::max(1u, cfg_.max_rois_per_frame), dcap = cfg_.det_cap, nv = n * R;
     const int L = cfg_.landmarker.num_landmarks, nkp = cfg_.detector.keypoints;
     const size_t nout = lc.nn().num_outputs();
     const Slot::Results &o = s.res[s.done];
-    const size_t roi0 = rois_.size();
-    std::vector<uint32_t> slot_of;  // the ROI slot of each result
+    const zr_track_state *state = reinterpret_cast<const zr_track_state *>(o.h_sum.ptr);
+    const zr_track_state *seed = state + nv;
+    const int32_t *count = reinterpret_cast<const int32_t *>(seed + nv);
+    std::vector<float> dets(n * dcap * 20), lmout(nv * L * 3), extra[2];
+    check(zr_memcpy_async(dets.data(), o.dets.ptr, dets.size() * 4, 1, nullptr));
+    check(zr_memcpy_async(lmout.data(), o.lmout.ptr, lmout.size() * 4, 1, nullptr));
+    for (size_t k = 2; k < nout && k < 4; k++) {  // handedness / world landmarks / tongue_out
+        extra[k - 2].resize((size_t)lc.nn().output_per_image(k) * nv);
+        check(zr_memcpy_async(extra[k - 2].data(), o.lm[k].ptr, extra[k - 2].size() * 4, 1, nullptr));
+    }
+    check(zr_stream_synchronize(nullptr));
     for (size_t i = 0; i < n; i++) {
         const size_t f = s.f0 + i;
-        const int cnt = o.dcount[i];
-        auto &dets = dets_[f];
-        dets.clear();
+        const int cnt = count[i];
+        auto &fd = dets_[f];
+        fd.clear();
         for (int k = 0; k < cnt && k < (int)dcap; k++) {
-            const float *e = &o.dets[(i * dcap + k) * 20];
+            const float *e = &dets[(i * dcap + k) * 20];
             Detection d;
             d.confidence = e[0];
             d.angle = e[1];
             d.rect = Rect::from_center(e[2], e[3], e[4], e[5]);
             for (int p = 0; p < nkp; p++) d.keypoints.push_back(Vec2{e[6 + 2 * p], e[7 + 2 * p]});
-            dets.push_back(std::move(d));
+            fd.push_back(std::move(d));
         }
         for (size_t k = 0; k < R; k++) {
-            const zr_track_state &s0 = o.seed[i * R + k];
+            const size_t v = i * R + k;
+            const zr_track_state &s0 = seed[v];
             if (!s0.active) continue;
             RoiResult r;
             r.frame = (uint32_t)f;
@@ -384,29 +391,25 @@ void DetectTrackPipeline::unpack_device(Slot &s) const {
             r.roi = RotatedRect(Rect::from_center(s0.roi[0], s0.roi[1], s0.roi[2], s0.roi[3]), s0.roi[4]);
             r.result.view_rect = RotatedRect(
                 Rect::from_center(s0.view_rect[0], s0.view_rect[1], s0.view_rect[2], s0.view_rect[3]), s0.view_rect[4]);
+            const zr_track_state &st = state[v];
+            r.confidence = st.confidence;
+            r.tracked = st.tracked != 0;
+            if (r.tracked) {
+                r.result.updated_roi = RotatedRect(
+                    Rect::from_center(st.updated[0], st.updated[1], st.updated[2], st.updated[3]), st.updated[4]);
+                r.next_roi = RotatedRect(Rect::from_center(st.roi[0], st.roi[1], st.roi[2], st.roi[3]), st.roi[4]);
+                Estimate &e = r.result.estimate;
+                const float *lm = &lmout[v * L * 3];
+                e.positions.assign(lm, lm + 3 * L);
+                e.confidence = st.confidence;
+                if (cfg_.landmarker.kind == NetworkKind::FaceMeshV2 && nout > 2) e.tongue_out = extra[0][v];
+                if (cfg_.landmarker.kind == NetworkKind::HandLandmarkLite && nout > 3) {
+                    e.raw_handedness = extra[0][v];
+                    const float *w = &extra[1][v * 3 * L];
+                    e.world.assign(w, w + 3 * L);
+                }
+            }
             rois_.push_back(std::move(r));
-            slot_of.push_back((uint32_t)(i * R + k));
-        }
-    }
-    for (size_t j = 0; j < slot_of.size(); j++) {
-        RoiResult &r = rois_[roi0 + j];
-        const size_t v = slot_of[j];
-        const zr_track_state &st = o.state[v];
-        r.confidence = st.confidence;
-        r.tracked = st.tracked != 0;
-        if (!r.tracked) continue;
-        r.result.updated_roi = RotatedRect(Rect::from_center(st.updated[0], st.updated[1], st.updated[2], st.updated[3]),
-                                           st.updated[4]);
-        r.next_roi = RotatedRect(Rect::from_center(st.roi[0], st.roi[1], st.roi[2], st.roi[3]), st.roi[4]);
-        Estimate &e = r.result.estimate;
-        const float *lm = &o.lmout[v * L * 3];
-        e.positions.assign(lm, lm + 3 * L);
-        e.confidence = st.confidence;
-        if (cfg_.landmarker.kind == NetworkKind::FaceMeshV2 && nout > 2) e.tongue_out = o.extra[0][v];
-        if (cfg_.landmarker.kind == NetworkKind::HandLandmarkLite && nout > 3) {
-            e.raw_handedness = o.extra[0][v];
-            const float *w = &o.extra[1][v * 3 * L];
-            e.world.assign(w, w + 3 * L);
         }
     }
 }
@@ -548,6 +551,7 @@ void DetectTrackPipeline::run(const std::vector<Image> &frames,
         s.f0 = f0;
         s.nf = B / S + (k < B % S ? 1 : 0);
         f0 += s.nf;
+        s.inputs_ok = false;  // new frames
         stage_detect(s, frames);
         if (cfg_.device_post) stage_device_post(s, frames, forced);
     }
@@ -599,6 +603,7 @@ void DetectTrackPipeline::begin_steps() {
         s.f0 = f0;
         s.nf = B / active_slots_ + (k < B % active_slots_ ? 1 : 0);
         f0 += s.nf;
+        s.inputs_ok = false;  // the slots' frame ranges may have changed
         stage_detect(s, frames);
         if (cfg_.device_post) stage_device_post(s, frames, forced_);
     }

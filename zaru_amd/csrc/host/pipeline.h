@@ -143,21 +143,23 @@ class DetectTrackPipeline {
         std::vector<zr_view> rv;
         std::vector<uint32_t> rf;
         size_t roi0 = 0, nroi = 0;
-        // device post-processing (PipelineConfig::device_post)
-        DeviceArray<float> d_lbox, d_forced, d_dets, d_lmout;
+        // device post-processing (PipelineConfig::device_post): per-frame inputs (uploaded once
+        // per frame set) ...
+        DeviceArray<float> d_lbox, d_forced;
         DeviceArray<uint32_t> d_fsize;
-        DeviceArray<int32_t> d_nforced, d_dcount;
-        DeviceArray<zr_track_state> d_state;
+        DeviceArray<int32_t> d_nforced;
         DeviceArray<zr_view_desc> d_views;
         PinnedArray<float> h_lbox, h_forced;
         PinnedArray<uint32_t> h_fsize;
         PinnedArray<int32_t> h_nforced;
-        // a step's results arrive in one of two host sets: the one a finished step filled is
-        // read (lazily, materialize()) while the next step's copies land in the other
+        bool inputs_ok = false;
+        // ... and two result sets on the device: a step writes one while the last finished
+        // step's stays readable.  Only the summary (tracker states, seeds, detection counts: one
+        // copy) comes to the host each step; detections and landmarks on demand (materialize)
         struct Results {
-            PinnedArray<int32_t> dcount;
-            PinnedArray<float> dets, lmout, extra[2];
-            PinnedArray<zr_track_state> seed, state;
+            DeviceArray<uint8_t> sum;  // [state: nv][seed: nv] zr_track_state, [count: n] int32
+            DeviceArray<float> dets, lmout, lm[4];
+            PinnedArray<uint8_t> h_sum;
         } res[2];
         int wr = 0;    // the set the enqueued step writes
         int done = 0;  // the set of the last finished step

@@ -1052,7 +1052,12 @@ const char *launch_dwpw(const DwPwParams &p, hipStream_t s) {
         if (p.k == 3) return p.stride == 1 ? dwpw_valu_co<3, 1>(p, s) : dwpw_valu_co<3, 2>(p, s);
         return p.stride == 1 ? dwpw_valu_co<5, 1>(p, s) : dwpw_valu_co<5, 2>(p, s);
     }
-    constexpr int64_t min_wgs = 1024;  // workgroups one launch should reach
+    // workgroups one launch should reach (ZARU_HIP_MINWGS overrides it for layout sweeps)
+    static const int64_t min_wgs = [] {
+        const char *e = std::getenv("ZARU_HIP_MINWGS");
+        const long v = e ? std::strtol(e, nullptr, 10) : 0;
+        return (int64_t)(v > 0 ? v : 1024);
+    }();
     const DwPwLayout *best = nullptr;
     int64_t best_wgs = 0;
     for (const DwPwLayout &l : kLayouts) {

@@ -223,6 +223,7 @@ __global__ __launch_bounds__(256) void seed_kernel(const SeedParams P) {
     }
     next_view(st, P.views[i], f, P.asp_w, P.asp_h);
     P.state[i] = st;
+    if (P.seed_copy) P.seed_copy[i] = st;
 }
 
 }  // namespace

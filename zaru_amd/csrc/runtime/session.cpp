@@ -698,7 +698,8 @@ int zr_detect_post_async(const float *d_logits, const float *d_boxes, const floa
 int zr_track_seed_detections_async(const int32_t *d_count, const float *d_dets, size_t dcap, const float *d_forced,
                                    const int32_t *d_nforced, const uint32_t *d_frame_size, size_t n,
                                    const zr_track_cfg *cfg, float roi_grow, int roi_use_angle,
-                                   zr_track_state *d_state, zr_view_desc *d_views, void *hip_stream) {
+                                   zr_track_state *d_state, zr_track_state *d_seed_copy, zr_view_desc *d_views,
+                                   void *hip_stream) {
     return guarded([&]() -> int {
         if (!d_count || !d_dets || !d_frame_size || !cfg || !d_state || !d_views || dcap == 0 ||
             (!d_forced != !d_nforced))
@@ -721,6 +722,7 @@ int zr_track_seed_detections_async(const int32_t *d_count, const float *d_dets, 
         p.asp_w = cfg->aspect_w;
         p.asp_h = cfg->aspect_h;
         p.state = reinterpret_cast<zr::TrackState *>(d_state);
+        p.seed_copy = reinterpret_cast<zr::TrackState *>(d_seed_copy);
         p.views = reinterpret_cast<zr::ViewDesc *>(d_views);
         zr::launch_seed(p, (hipStream_t)hip_stream);
         HIP_TRY(hipGetLastError());

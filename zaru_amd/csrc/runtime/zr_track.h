@@ -75,6 +75,7 @@ struct SeedParams {
     int roi_use_angle;
     int asp_w, asp_h;
     TrackState *state;       // [N * R] out
+    TrackState *seed_copy;   // [N * R] out, may be null: the seeds again (the update rewrites state)
     ViewDesc *views;         // [N * R] out
 };
 const char *launch_seed(const SeedParams &p, hipStream_t s);
