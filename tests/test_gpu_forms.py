@@ -40,6 +40,7 @@ SWITCHES = {
     "no_rows": "-rows",
     "no_vres": "-vres",
     "no_vstore": "-vstore",
+    "ring": "+ring",  # persistent LDS-ring MFMA dwpw (dwpw_mfma.hip), opt-in
     "chain": "+chain",  # low-resolution layer runs in one launch per image (chain.hip)
     "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore",
 }

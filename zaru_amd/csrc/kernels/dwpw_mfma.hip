@@ -1,0 +1,958 @@
+// dwpw_mfma.hip -- the depthwise KxK -> 1x1 BlazeBlock (inverted-residual tail) as one launch
+// for the low-resolution, many-channel layers: the depthwise output of a column tile lives only
+// in LDS and feeds an f32 MFMA GEMM (v_mfma_f32_32x32x2_f32, exact f32) whose epilogue applies
+// bias, activation, residual (+pad/+pool) and activation.
+// Reference: the Conv nodes of the four ONNX graphs that ORT/tract execute at
+// crates/zaru/src/nn/mod.rs:483-533 (the BlazeBlocks).
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
+#include "../runtime/zr_kernels.h"
+#include "act.h"
+#include "epilogue.h"
+#include "lds_dma.h"
+
+namespace zr {
+
+// A workgroup (4 waves) owns a BM x BN output tile: BN consecutive columns j = n*P + q of the
+// 1x1 conv's output and BM of its output channels.  The waves are laid out WM along M and
+// 4/WM along N; each wave holds MTW x NTW 32x32 accumulator tiles.  Per chunk of FKC input
+// channels:
+//   1. the workgroup computes the depthwise outputs of the chunk for its BN columns into LDS
+//      (taps straight from L1/L2, where neighbouring columns share them; every tap of the
+//      chunk is issued before the first is used; clamped addresses + a validity mask, never a
+//      branch around a load);
+//   2. the chunk of the transposed 1x1 weights goes to LDS;
+//   3. every wave runs v_mfma_f32_32x32x2_f32 over the chunk.
+// The epilogue is epilogue_tile: bias, activation, residual (+pad/+pool), activation.
+// The layout is chosen per layer (launch_dwpw) so that a launch has enough workgroups to fill
+// 256 CUs without splitting M (which would recompute the depthwise part): wide column tiles
+// for the few-channel high-resolution layers, tall channel tiles for the 128/256-channel
+// low-resolution ones.  Column tiles are dealt to XCDs in contiguous runs, so halo rows and the
+// residual re-read are L2 hits on the XCD that just fetched them.
+// V4: the depthwise part computes 4 horizontally adjacent outputs per thread from one input
+// window per row (float4 loads plus pad_l scalars) instead of K*K lane-private taps per
+// output: ~4x fewer memory instructions.  Needs OW % 4 == 0, W % 4 == 0 and the models'
+// TF-style pads (K3: 1 for stride 1, 0 for stride 2; K5: 2 / 1) -- see v4_ok().
+
+template <int K, int S, int WM, int MTW, int NTW, bool V4>
+__global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) {
+    constexpr int WN = 4 / WM;
+    constexpr int BN = WN * NTW * 32, BM = WM * MTW * 32;
+    constexpr int KK = K * K;
+    constexpr int FKC = K == 3 ? 16 : 8;  // input channels per chunk
+    constexpr int CPAR = 256 / BN;        // channels whose depthwise runs side by side
+    constexpr int PER = FKC / CPAR;       // depthwise outputs per thread per chunk
+    static_assert(PER >= 1 && FKC % CPAR == 0, "tile/chunk mismatch");
+    // V4 layout: Q column quads x CS channel slots; CPT channels per thread
+    constexpr int Q = BN / 4, CS = 256 / Q, CPT = FKC > CS ? FKC / CS : 1;
+    constexpr int PL = DwPad<K, S>::L;
+    constexpr int NV = (3 * S + K - PL + 3) / 4;  // float4 loads per window row
+    constexpr int WL = PL + 4 * NV;               // window floats per row
+    __shared__ __attribute__((aligned(16))) float sD[FKC][BN];
+    __shared__ float sW[FKC][BM];
+    const GemmParams &G = P.g;
+
+    const int cpx = gridDim.x >> 3;  // gridDim.x is a multiple of 8
+    const int tile = (blockIdx.x & 7) * cpx + (blockIdx.x >> 3);
+    if (tile >= nct) return;  // whole workgroup, before any barrier
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kh = lane >> 5, col = lane & 31;
+    const int wm = wave % WM, wn = wave / WM;
+    const int j0 = tile * BN, m0 = blockIdx.y * BM;
+    const int Cin = G.K;
+
+    // depthwise role: column dj of the tile, channels dc, dc + CPAR, ... of each chunk
+    const int dj = tid % BN;
+    int dc = tid / BN;
+    if constexpr (BN >= 64) dc = __builtin_amdgcn_readfirstlane(dc);  // one channel per wave
+    const int jd = min(j0 + dj, G.ncols - 1);
+    const int n = jd / G.P, q = jd - n * G.P;
+    const int oy = q / P.OW, ox = q - oy * P.OW;
+    const int iy0 = oy * S - P.pad_t, ix0 = ox * S - P.pad_l;
+    const int H = P.in.H, W = P.in.W;
+    // tap byte offsets from a channel plane's base, image included (32-bit: see epilogue.h)
+    const uint32_t nbase = (uint32_t)n * (uint32_t)P.in.sN;
+    uint32_t off[KK];
+    uint32_t mask = 0;
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) {
+            const int iy = iy0 + ky, ix = ix0 + kx;
+            const bool ok = iy >= 0 && iy < H && ix >= 0 && ix < W;
+            off[ky * K + kx] = (nbase + (ok ? (uint32_t)(iy * W + ix) : 0u)) * 4u;  // bytes
+            mask |= (ok ? 1u : 0u) << (ky * K + kx);
+        }
+
+    // V4 role: column quad qd (positions j4 .. j4+3 of one image row), channel slot cs
+    const int qd = tid % Q, cs = tid / Q;
+    const int j4 = min(j0 + 4 * qd, G.ncols - 4);
+    const int n4 = j4 / G.P, q4 = j4 - n4 * G.P;
+    const int oy4 = q4 / P.OW, ox4 = q4 - oy4 * P.OW;
+    const int a4 = ox4 * S;  // 16-byte aligned window start (W % 4 == 0, ox4 % 4 == 0)
+    const uint32_t nbase4 = (uint32_t)n4 * (uint32_t)P.in.sN;
+
+    f32x16 acc[MTW][NTW];
+#pragma unroll
+    for (int t = 0; t < MTW; ++t)
+#pragma unroll
+        for (int u = 0; u < NTW; ++u)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
+
+    // Software pipeline over the channel chunks: the taps and 1x1 weights of chunk k+1 are
+    // loaded into registers while the waves run chunk k's MFMAs, so the global-load latency of
+    // every chunk after the first hides behind matrix work.
+    constexpr int WPT = (FKC * BM + 255) / 256;  // 1x1 weights staged per thread per chunk
+    float tap[V4 ? 1 : PER][V4 ? 1 : KK], win[V4 ? CPT : 1][V4 ? K : 1][V4 ? WL : 1], wreg[WPT];
+    auto load_chunk = [&](int kc) {
+        if constexpr (V4) {
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int c = kc + cs + CS * i;
+                const float *pl = P.in.p + (size_t)(uint32_t)(c < Cin ? c : Cin - 1) * (uint32_t)P.in.sC + nbase4;
+#pragma unroll
+                for (int ky = 0; ky < K; ++ky) {
+                    const int iy = oy4 * S - P.pad_t + ky;
+                    const bool rok = iy >= 0 && iy < H;
+                    const uint32_t rb = (uint32_t)(rok ? iy : 0) * (uint32_t)W;
+#pragma unroll
+                    for (int e = 0; e < PL; ++e) {  // left of the aligned part
+                        const int x = a4 - PL + e;
+                        const float v = pl[rb + (uint32_t)(x >= 0 ? x : 0)];
+                        win[i][ky][e] = rok && x >= 0 ? v : 0.f;
+                    }
+#pragma unroll
+                    for (int v4 = 0; v4 < NV; ++v4) {
+                        const int x = a4 + 4 * v4;
+                        const bool ok = rok && x < W;
+                        const float4 v = *(const float4 *)(pl + rb + (uint32_t)(ok ? x : 0));
+                        win[i][ky][PL + 4 * v4 + 0] = ok ? v.x : 0.f;
+                        win[i][ky][PL + 4 * v4 + 1] = ok ? v.y : 0.f;
+                        win[i][ky][PL + 4 * v4 + 2] = ok ? v.z : 0.f;
+                        win[i][ky][PL + 4 * v4 + 3] = ok ? v.w : 0.f;
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int c = kc + dc + CPAR * i;
+                const char *pl = (const char *)(P.in.p + (size_t)(uint32_t)(c < Cin ? c : Cin - 1) * (uint32_t)P.in.sC);
+#pragma unroll
+                for (int t = 0; t < KK; ++t) tap[i][t] = *(const float *)(pl + off[t]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < WPT; ++u) {
+            const int i = min(tid + 256 * u, FKC * BM - 1);
+            const int r = i / BM, cc = i - r * BM;
+            const int k = kc + r, m = m0 + cc;
+            const float x = G.wt[(int64_t)(k < Cin ? k : Cin - 1) * G.Mpad + (m < G.Mpad ? m : 0)];
+            wreg[u] = (k < Cin && m < G.Mpad) ? x : 0.f;
+        }
+    };
+    load_chunk(0);
+    for (int kc = 0; kc < Cin; kc += FKC) {
+        if constexpr (V4) {
+            float dv[CPT * 4];
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int c = kc + cs + CS * i;
+                const int cl = c < Cin ? c : Cin - 1;
+                const float *w = P.dw_w + cl * KK;
+                const float b = P.dw_b[cl];
+#pragma unroll
+                for (int o = 0; o < 4; ++o) {
+                    float a = b;
+#pragma unroll
+                    for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+                        for (int kx = 0; kx < K; ++kx) a = __builtin_fmaf(w[ky * K + kx], win[i][ky][o * S + kx], a);
+                    dv[4 * i + o] = a;
+                }
+            }
+            apply_act_n<CPT * 4>(P.dw_act, dv, [&](int e) {
+                const int c = kc + cs + CS * (e >> 2);
+                return c < Cin ? c : Cin - 1;
+            });
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int c = cs + CS * i;
+                if (c < FKC) {
+                    const bool ok = kc + c < Cin;
+                    *(float4 *)&sD[c][4 * qd] = make_float4(ok ? dv[4 * i] : 0.f, ok ? dv[4 * i + 1] : 0.f,
+                                                            ok ? dv[4 * i + 2] : 0.f, ok ? dv[4 * i + 3] : 0.f);
+                }
+            }
+        } else {
+            float dv[PER];
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int c = kc + dc + CPAR * i;
+                const int cl = c < Cin ? c : Cin - 1;
+                const float *w = P.dw_w + cl * KK;
+                float a = P.dw_b[cl];
+#pragma unroll
+                for (int t = 0; t < KK; ++t) a = __builtin_fmaf(w[t], ((mask >> t) & 1u) ? tap[i][t] : 0.f, a);
+                dv[i] = a;
+            }
+            apply_act_n<PER>(P.dw_act, dv, [&](int i) {
+                const int c = kc + dc + CPAR * i;
+                return c < Cin ? c : Cin - 1;
+            });
+#pragma unroll
+            for (int i = 0; i < PER; ++i) sD[dc + CPAR * i][dj] = kc + dc + CPAR * i < Cin ? dv[i] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < WPT; ++u) {
+            const int i = tid + 256 * u;
+            if (i < FKC * BM) (&sW[0][0])[i] = wreg[u];
+        }
+        __syncthreads();
+        if (kc + FKC < Cin) load_chunk(kc + FKC);
+#pragma unroll
+        for (int s = 0; s < FKC / 2; ++s) {
+            float a[MTW], b[NTW];
+#pragma unroll
+            for (int t = 0; t < MTW; ++t) a[t] = sW[2 * s + kh][(wm * MTW + t) * 32 + col];
+#pragma unroll
+            for (int u = 0; u < NTW; ++u) b[u] = sD[2 * s + kh][(wn * NTW + u) * 32 + col];
+#pragma unroll
+            for (int t = 0; t < MTW; ++t)
+#pragma unroll
+                for (int u = 0; u < NTW; ++u)
+                    acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t], b[u], acc[t][u], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+
+#pragma unroll
+    for (int u = 0; u < NTW; ++u) {
+        const int j = j0 + (wn * NTW + u) * 32 + col;
+        if (j >= G.ncols) continue;
+        const int on = j / G.P, oq = j - on * G.P;
+#pragma unroll
+        for (int t = 0; t < MTW; ++t) epilogue_tile(G, acc[t][u], on, oq, m0 + (wm * MTW + t) * 32, kh);
+    }
+}
+
+
+// LDS-DMA form of the MFMA dwpw for the low-resolution layers (24^2 ... 3^2 planes with 64-256
+// channels), whose register-staged form waits on memory most of the time.  Per chunk of DFKC
+// input channels one LDS buffer receives, by global_load_lds_dwordx4 (no VGPRs, no staging
+// instructions beyond the address math), the contiguous CNHW run of input each channel needs for
+// the tile's BN columns (images are contiguous inside a channel: the run from the first needed
+// row of the first image to the last needed row of the last one) and the chunk's depthwise
+// weights and biases.  Two buffers: the next chunk's copy is in flight while this chunk's
+// depthwise (from LDS) and MFMAs run; the barrier that publishes the depthwise tile to the MFMAs
+// is a bare s_barrier, so it does not drain that copy.
+// WREG (MTW == 1): the 1x1 weights (the MFMA A operand) do not pass through LDS: each wave loads
+// its own 32-row slice of the chunk's transposed weights into registers one chunk ahead
+// (coalesced 128-B rows, L2 hits -- every workgroup reads the same few KiB).  Staged in LDS they
+// are ~60 % of a chunk's copy; in registers they leave room for 32-channel chunks at the same
+// occupancy.  With MTW = 2 the two register sets would cost a wave per SIMD, so
+// those layouts stage the weights' chunk rows in the DMA buffer.
+// (MTW == 1: 4 waves per SIMD fit in 128 registers without spills)
+template <int K, int S, int WM, int MTW, int DFKC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTW == 1 ? 4 : 1)))
+void dwpw_dma_kernel(const DwPwParams P, int nct, int runmax, int bufsz) {
+    constexpr int WN = 4 / WM, BN = WN * 32, BM = WM * MTW * 32, KK = K * K;
+    constexpr int CPAR = 256 / BN, PER = DFKC / CPAR;
+    constexpr int KKP = (DFKC * KK + 3) / 4 * 4;
+    constexpr bool WREG = MTW == 1;
+    // [guard: 256 words] [2 x bufsz] [sD: DFKC x BN]; masked taps of the first run may index up
+    // to pad_t * W + pad_l words before it, into the guard rather than out of the allocation
+    extern __shared__ __attribute__((aligned(16))) float lds_all[];
+    float *smem = lds_all + 256;
+    float *sD = smem + 2 * bufsz;
+    const GemmParams &G = P.g;
+
+    const int cpx = gridDim.x >> 3;  // gridDim.x is a multiple of 8
+    const int tile = (blockIdx.x & 7) * cpx + (blockIdx.x >> 3);
+    if (tile >= nct) return;  // whole workgroup, before any barrier
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kh = lane >> 5, col = lane & 31;
+    const int wm = wave % WM, wn = wave / WM;
+    const int j0 = tile * BN, m0 = blockIdx.y * BM;
+    const int Cin = G.K, H = P.in.H, W = P.in.W, Pin = H * W, OW = P.OW, Pq = G.P;
+    const int pt = P.pad_t, pl = P.pad_l;
+
+    // the input run of this tile (floats from a channel's base; 16-byte aligned ends)
+    const int ja = j0, jb = min(j0 + BN, G.ncols) - 1;
+    const int na = ja / Pq, qa = ja - na * Pq, nb = jb / Pq, qb = jb - nb * Pq;
+    const int ya = max(qa / OW * S - pt, 0), yb = min(qb / OW * S - pt + K - 1, H - 1);
+    const int s0 = (na * Pin + ya * W) & ~3;
+    const int e0 = (nb * Pin + (yb + 1) * W + 3) & ~3;
+    const int run4 = (e0 - s0) >> 2;  // <= runmax / 4
+
+    // slot regions of a buffer (16-byte slots): input runs | 1x1 weight rows (!WREG) |
+    // depthwise weights | biases
+    const int rq = runmax >> 2;
+    const int r1 = DFKC * rq, r2 = r1 + (WREG ? 0 : DFKC * (BM / 4)), r3 = r2 + KKP / 4, r4 = r3 + DFKC / 4;
+    const float inv_rq = 1.f / (float)rq;
+    const int nwi = bufsz >> 8;  // 64-slot DMA wave-instructions per buffer
+    auto stage = [&](int kc, float *dst) {
+        for (int wi = wave; wi < nwi; wi += 4) {
+            const int sl = wi * 64 + lane;
+            const float *src = (const float *)&zr_zero4;
+            if (sl < r1) {
+                const int c = qdiv(sl, rq, inv_rq), i = sl - c * rq;
+                if (kc + c < Cin && i < run4)
+                    src = P.in.p + (size_t)(uint32_t)(kc + c) * (uint32_t)P.in.sC + (uint32_t)(s0 + 4 * i);
+            } else if (sl < r2) {
+                const int r = (sl - r1) / (BM / 4), i = sl - r1 - r * (BM / 4);
+                if (kc + r < G.Kpad && m0 + 4 * i < G.Mpad)
+                    src = G.wt + (size_t)(uint32_t)(kc + r) * (uint32_t)G.Mpad + (uint32_t)(m0 + 4 * i);
+            } else if (sl < r3) {
+                const int i = sl - r2;
+                if (kc * KK + 4 * i < Cin * KK) src = P.dw_w + kc * KK + 4 * i;
+            } else if (sl < r4) {
+                const int i = sl - r3;
+                if (kc + 4 * i < Cin) src = P.dw_b + kc + 4 * i;
+            }
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                             (__attribute__((address_space(3))) void *)(dst + wi * 256), 16, 0, 0);
+        }
+    };
+    // this lane's A fragments of a chunk: W^T[kc + 2s + kh][row t*32 + col of the wave's slice];
+    // rows past Kpad / Mpad are the zero padding (clamped address + select, no branch)
+    const int mw = m0 + wm * MTW * 32 + col;
+    constexpr int WT = WREG ? MTW : 1, WS = WREG ? DFKC / 2 : 1;
+    auto wload = [&](int kc, float (&w)[WT][WS]) {
+        if constexpr (!WREG) return;
+#pragma unroll
+        for (int s = 0; s < DFKC / 2; ++s) {
+            const int k = kc + 2 * s + kh;
+#pragma unroll
+            for (int t = 0; t < MTW; ++t) {
+                const bool ok = k < G.Kpad && mw + t * 32 < G.Mpad;
+                const float x = G.wt[ok ? (uint32_t)k * (uint32_t)G.Mpad + (uint32_t)(mw + t * 32) : 0u];
+                w[t][s] = ok ? x : 0.f;
+            }
+        }
+    };
+
+    // depthwise role: column dj, channels dc, dc + CPAR, ... of each chunk
+    const int dj = tid % BN;
+    int dc = tid / BN;
+    if constexpr (BN >= 64) dc = __builtin_amdgcn_readfirstlane(dc);  // one channel per wave
+    const int jd = min(j0 + dj, G.ncols - 1);
+    const int n = jd / Pq, q = jd - n * Pq;
+    const int oy = q / OW, ox = q - oy * OW;
+    const int iy0 = oy * S - pt, ix0 = ox * S - pl;
+    const int tb = n * Pin + iy0 * W + ix0 - s0;  // run index of tap (0, 0) (may be < 0 when masked)
+    uint32_t mask = 0;
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) {
+            const int iy = iy0 + ky, ix = ix0 + kx;
+            mask |= (iy >= 0 && iy < H && ix >= 0 && ix < W ? 1u : 0u) << (ky * K + kx);
+        }
+
+    f32x16 acc[MTW];
+#pragma unroll
+    for (int t = 0; t < MTW; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+    float wa[WT][WS], wnx[WT][WS];
+    stage(0, smem);
+    wload(0, wa);
+    for (int kc = 0, it = 0; kc < Cin; kc += DFKC, ++it) {
+        const float *buf = smem + (it & 1) * bufsz;
+        __syncthreads();  // vmcnt(0) + barrier: this chunk has landed; last chunk's readers are done
+        if (kc + DFKC < Cin) {
+            stage(kc + DFKC, smem + ((it + 1) & 1) * bufsz);
+            wload(kc + DFKC, wnx);
+        }
+        const float *sIn = buf, *sW = buf + DFKC * runmax, *sDW = sW + (WREG ? 0 : DFKC * BM), *sDB = sDW + KKP;
+        float dv[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int c = dc + CPAR * i;
+            const float *t0 = sIn + c * runmax + tb;
+            const float *w = sDW + c * KK;
+            float a = sDB[c];
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx) {
+                    const int t = ky * K + kx;
+                    const float x = t0[ky * W + kx];
+                    a = __builtin_fmaf(w[t], ((mask >> t) & 1u) ? x : 0.f, a);
+                }
+            dv[i] = a;
+        }
+        apply_act_n<PER>(P.dw_act, dv, [&](int i) {
+            const int c = kc + dc + CPAR * i;
+            return c < Cin ? c : Cin - 1;
+        });
+#pragma unroll
+        for (int i = 0; i < PER; ++i) sD[(dc + CPAR * i) * BN + dj] = kc + dc + CPAR * i < Cin ? dv[i] : 0.f;
+        // publish sD without draining the next chunk's DMA and weight loads (a __syncthreads
+        // would wait vmcnt(0))
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+        for (int s = 0; s < DFKC / 2; ++s) {
+            const float b = sD[(2 * s + kh) * BN + wn * 32 + col];
+#pragma unroll
+            for (int t = 0; t < MTW; ++t) {
+                float a;
+                if constexpr (WREG) a = wa[t][s];
+                else a = sW[(2 * s + kh) * BM + (wm * MTW + t) * 32 + col];
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[t], 0, 0, 0);
+            }
+        }
+        if constexpr (WREG) {
+#pragma unroll
+            for (int t = 0; t < WT; ++t)
+#pragma unroll
+                for (int s = 0; s < WS; ++s) wa[t][s] = wnx[t][s];
+        }
+    }
+
+    const int j = j0 + wn * 32 + col;
+    if (j >= G.ncols) return;
+    const int on = j / Pq, oq = j - on * Pq;
+#pragma unroll
+    for (int t = 0; t < MTW; ++t) epilogue_tile(G, acc[t], on, oq, m0 + (wm * MTW + t) * 32, kh);
+}
+
+// ------------------------------------------------------------------ persistent LDS-ring form
+// The low-resolution BlazeBlocks are a small GEMM (M, K <= 128..256) behind a depthwise
+// prologue, over many columns.  Per tile of BN columns the per-chunk form above pays a dependent
+// HBM round trip for every 16-channel chunk, re-stages the layer's 1x1 weights for every tile
+// (60 % of each chunk's LDS copy), fences its epilogue behind residual / bias loads, and runs
+// its depthwise and MFMA phases back to back.  Measured per phase (tools/debug):
+// MFMA busy < 25 %, and a tile's fixed costs (index math, barriers, epilogue) repeat per 8
+// chunks.  This form instead:
+//   * is persistent: one 512-thread workgroup per CU (8 waves, WM along M x 8/WM along N) walks
+//     a run of column tiles (contiguous runs per XCD, so halo rows are L2 hits);
+//   * stages the whole layer's 1x1 weights, depthwise weights / biases, the epilogue bias and
+//     the activation slopes in LDS once per workgroup;
+//   * streams the activation runs through a ring of D LDS stages by LDS-DMA, D - 1 chunks ahead
+//     across tile boundaries, waiting with a counted vmcnt for exactly the stage it needs (the
+//     DMA count per wave and stage is fixed, and nothing else in the loop loads to VGPRs);
+//   * software-pipelines the chunk loop: in one barrier interval the waves compute chunk g + 1's
+//     depthwise into one of two depthwise tiles while the MFMAs consume chunk g from the other;
+//   * takes the block's residual from the staged taps (the centre tap, or the 2x2 max-pool of
+//     the taps at stride 2) into a second pair of tiles, which the MFMA phase moves into the
+//     lanes' accumulator layout -- the epilogue reads no global memory.
+// Same arithmetic in the same order as dwpw_dma_kernel / dwpw_kernel: bitwise equal.
+constexpr int RING_DFKC = 16;
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate is a compile-time field)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+    switch (__builtin_amdgcn_readfirstlane(n)) {
+#define ZR_VMW(i) case i: asm volatile("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
+        ZR_VMW(0) ZR_VMW(1) ZR_VMW(2) ZR_VMW(3) ZR_VMW(4) ZR_VMW(5) ZR_VMW(6) ZR_VMW(7)
+        ZR_VMW(8) ZR_VMW(9) ZR_VMW(10) ZR_VMW(11) ZR_VMW(12) ZR_VMW(13) ZR_VMW(14) ZR_VMW(15)
+        ZR_VMW(16) ZR_VMW(17) ZR_VMW(18) ZR_VMW(19) ZR_VMW(20) ZR_VMW(21) ZR_VMW(22) ZR_VMW(23)
+        ZR_VMW(24) ZR_VMW(25) ZR_VMW(26) ZR_VMW(27) ZR_VMW(28) ZR_VMW(29) ZR_VMW(30) ZR_VMW(31)
+        ZR_VMW(32) ZR_VMW(33) ZR_VMW(34) ZR_VMW(35) ZR_VMW(36) ZR_VMW(37) ZR_VMW(38) ZR_VMW(39)
+        ZR_VMW(40) ZR_VMW(41) ZR_VMW(42) ZR_VMW(43) ZR_VMW(44) ZR_VMW(45) ZR_VMW(46) ZR_VMW(47)
+        ZR_VMW(48) ZR_VMW(49) ZR_VMW(50) ZR_VMW(51) ZR_VMW(52) ZR_VMW(53) ZR_VMW(54) ZR_VMW(55)
+        ZR_VMW(56) ZR_VMW(57) ZR_VMW(58) ZR_VMW(59) ZR_VMW(60) ZR_VMW(61) ZR_VMW(62)
+#undef ZR_VMW
+    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
+    }
+}
+
+// activation of N values with their per-channel slopes in LDS (PReLU); same arithmetic as
+// apply_act_n, the uniform switch outside the element loop
+template <int N, typename ChanFn>
+__device__ __forceinline__ void ring_act_n(int kind, float lo, float hi, const float *slope, float *v, ChanFn ch) {
+    switch (kind) {
+    case ACT_RELU:
+#pragma unroll
+        for (int r = 0; r < N; ++r) v[r] = fmaxf(v[r], 0.f);
+        break;
+    case ACT_CLIP:
+#pragma unroll
+        for (int r = 0; r < N; ++r) v[r] = fminf(fmaxf(v[r], lo), hi);
+        break;
+    case ACT_PRELU:
+#pragma unroll
+        for (int r = 0; r < N; ++r) v[r] = v[r] < 0.f ? v[r] * slope[ch(r)] : v[r];
+        break;
+    case ACT_SIGMOID:
+#pragma unroll
+        for (int r = 0; r < N; ++r) v[r] = 1.f / (1.f + expf(-v[r]));
+        break;
+    default: break;
+    }
+}
+
+// Launch-time layout of one ring launch (host-computed, passed by value).
+struct RingPlan {
+    int nct;          // column tiles
+    int nch;          // channel chunks (RING_DFKC each)
+    int rq;           // 16-B slots per channel in a stage (the longest tile run)
+    int stg;          // floats per stage (whole 1 KiB DMA wave-instructions)
+    int D;            // ring depth
+    int tpx;          // tiles per XCD range
+    int res;          // residual from the staged taps: 0 none, 1 centre tap, 2 2x2 max-pool
+    // LDS offsets (floats)
+    int o_ring, o_w, o_dw, o_db, o_b, o_spre, o_spost, o_sdw, o_d, o_r, lds_floats;
+    int dbg;
+};
+
+template <int K, int S, int WM>
+__global__ __launch_bounds__(512) void dwpw_ring_kernel(const DwPwParams P, const RingPlan R) {
+    constexpr int NW = 8, WN = NW / WM, BN = WN * 32, BM = WM * 32, KK = K * K, FK = RING_DFKC;
+    constexpr int CPAR = 512 / BN, PER = FK / CPAR;
+    constexpr int PL = DwPad<K, S>::L;  // the residual taps (the host checks the pads are these)
+    static_assert(PER >= 1 && FK % CPAR == 0, "tile / chunk mismatch");
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const GemmParams &G = P.g;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kh = lane >> 5, col = lane & 31;
+    const int wm = wave % WM, wn = wave / WM;
+
+    // this workgroup's tiles: XCD x owns tiles [x * tpx, (x + 1) * tpx); its G8 workgroups take
+    // them round robin
+    const int G8 = gridDim.x >> 3, xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int t_beg = xcd * R.tpx + slot, t_end = min((xcd + 1) * R.tpx, R.nct);
+    const int ntl = t_beg < t_end ? (t_end - t_beg + G8 - 1) / G8 : 0;
+    if (ntl == 0) return;  // whole workgroup, before any barrier
+    const int nstages = ntl * R.nch;
+    const int Cin = G.K, H = P.in.H, W = P.in.W, Pin = H * W, OW = P.OW, Pq = G.P;
+    const int pt = P.pad_t, pl = P.pad_l, Mpad = G.Mpad;
+    float *ring = lds + R.o_ring, *sW = lds + R.o_w, *sDW = lds + R.o_dw, *sDB = lds + R.o_db;
+    float *sB = lds + R.o_b, *sPre = lds + R.o_spre, *sPost = lds + R.o_spost, *sDS = lds + R.o_sdw;
+    float *sD = lds + R.o_d, *sR = lds + R.o_r;
+    constexpr int DS = BN;  // depthwise-tile row stride
+
+    // ---- once per workgroup: weights, depthwise parameters, bias and slopes into LDS
+    if (!(R.dbg & 16)) {
+        const int kr = R.nch * FK;  // weight rows staged (rows >= Kpad are zero)
+        const int n4 = kr * Mpad / 4;
+        for (int i = tid; i < n4; i += 512) {
+            const int k = (4 * i) / Mpad, m = 4 * i - k * Mpad;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (k < G.Kpad) v = *reinterpret_cast<const float4 *>(G.wt + (size_t)k * Mpad + m);
+            *reinterpret_cast<float4 *>(sW + 4 * i) = v;
+        }
+        for (int i = tid; i < kr * KK; i += 512) sDW[i] = i < Cin * KK ? P.dw_w[i] : 0.f;
+        for (int i = tid; i < kr; i += 512) {
+            sDB[i] = i < Cin ? P.dw_b[i] : 0.f;
+            sDS[i] = (P.dw_act.kind == ACT_PRELU && i < Cin) ? P.dw_act.slope[i] : 0.f;
+        }
+        for (int i = tid; i < Mpad; i += 512) {
+            sB[i] = G.bias[i];
+            sPre[i] = (G.pre.kind == ACT_PRELU && i < G.M) ? G.pre.slope[i] : 0.f;
+            sPost[i] = (G.post.kind == ACT_PRELU && i < G.M) ? G.post.slope[i] : 0.f;
+        }
+    }
+
+    // ---- the DMA of stage q (tile t_beg + (q / nch) * G8, chunk q % nch) into ring slot
+    const int nwi = R.stg >> 8;                                      // wave-instructions per stage
+    const int cnt_w = wave < nwi ? (nwi - wave + NW - 1) / NW : 0;  // of them issued by this wave
+    const float inv_rq = 1.f / (float)R.rq;
+    auto tile_of = [&](int q) { return t_beg + (q / R.nch) * G8; };
+    auto run_of = [&](int t, int &s0, int &run4) {
+        const int ja = t * BN, jb = min(ja + BN, G.ncols) - 1;
+        const int na = ja / Pq, qa = ja - na * Pq, nb = jb / Pq, qb = jb - nb * Pq;
+        const int ya = max(qa / OW * S - pt, 0), yb = min(qb / OW * S - pt + K - 1, H - 1);
+        s0 = (na * Pin + ya * W) & ~3;
+        run4 = (((nb * Pin + (yb + 1) * W + 3) & ~3) - s0) >> 2;
+    };
+    auto issue = [&](int q, int rs) {
+        const int t = tile_of(q), kc = (q % R.nch) * FK;
+        int s0, run4;
+        run_of(t, s0, run4);
+        float *dst = ring + rs * R.stg;
+        if (R.dbg & 4) return;
+        for (int wi = wave; wi < nwi; wi += NW) {
+            const int sl = wi * 64 + lane;
+            const int c = qdiv(sl, R.rq, inv_rq), i = sl - c * R.rq;
+            const float *src = (const float *)&zr_zero4;
+            if (c < FK && kc + c < Cin && i < run4)
+                src = P.in.p + (size_t)(uint32_t)(kc + c) * (uint32_t)P.in.sC + (uint32_t)(s0 + 4 * i);
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                             (__attribute__((address_space(3))) void *)(dst + wi * 256), 16, 0, 0);
+        }
+    };
+
+    // ---- depthwise role: column dj of the tile, channels dc + CPAR * i of each chunk
+    const int dj = tid % BN;
+    int dc = tid / BN;
+    if constexpr (BN >= 64) dc = __builtin_amdgcn_readfirstlane(dc);  // one channel per wave
+    int d_tile = -1, d_s0 = 0, d_tb = 0;
+    uint32_t d_mask = 0;
+    // chunk of stage q: depthwise (+ residual taps) from its ring slot into tile buffer db
+    auto depthwise = [&](int q, int rs, int db) {
+        const int t = tile_of(q), kc = (q % R.nch) * FK;
+        if (t != d_tile) {  // per-tile geometry of this thread's column
+            d_tile = t;
+            int run4;
+            run_of(t, d_s0, run4);
+            const int jd = min(t * BN + dj, G.ncols - 1);
+            const int n = jd / Pq, qq = jd - n * Pq;
+            const int oy = qq / OW, ox = qq - oy * OW;
+            const int iy0 = oy * S - pt, ix0 = ox * S - pl;
+            d_tb = n * Pin + iy0 * W + ix0 - d_s0;
+            d_mask = 0;
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx) {
+                    const int iy = iy0 + ky, ix = ix0 + kx;
+                    d_mask |= (iy >= 0 && iy < H && ix >= 0 && ix < W ? 1u : 0u) << (ky * K + kx);
+                }
+        }
+        const float *stage = ring + rs * R.stg;
+        if (R.dbg & 2) return;
+        float x[PER][KK];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const float *t0 = stage + (dc + CPAR * i) * (R.rq * 4) + d_tb;
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx) x[i][ky * K + kx] = t0[ky * W + kx];
+        }
+        float dv[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int c = kc + dc + CPAR * i;
+            const float *w = sDW + c * KK;
+            float a = sDB[c];
+#pragma unroll
+            for (int t = 0; t < KK; ++t) a = __builtin_fmaf(w[t], ((d_mask >> t) & 1u) ? x[i][t] : 0.f, a);
+            dv[i] = a;
+        }
+        ring_act_n<PER>(P.dw_act.kind, P.dw_act.lo, P.dw_act.hi, sDS, dv, [&](int i) {
+            const int c = kc + dc + CPAR * i;
+            return c < Cin ? c : Cin - 1;
+        });
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int c = kc + dc + CPAR * i;
+            sD[db * FK * DS + (dc + CPAR * i) * DS + dj] = c < Cin ? dv[i] : 0.f;
+            if (R.res) {
+                float r;
+                if constexpr (S == 1) {
+                    r = x[i][PL * K + PL];
+                } else {
+                    r = fmaxf(fmaxf(x[i][PL * K + PL], x[i][PL * K + PL + 1]),
+                              fmaxf(x[i][(PL + 1) * K + PL], x[i][(PL + 1) * K + PL + 1]));
+                }
+                sR[db * FK * DS + (dc + CPAR * i) * DS + dj] = c < G.r_C ? r : 0.f;
+            }
+        }
+    };
+
+    // ---- prologue: parameters visible, first D stages in flight, chunk 0's depthwise
+    int issued = min(R.D, nstages);
+    for (int q = 0; q < issued; ++q) issue(q, q);
+    __syncthreads();  // the parameter stores (and, through vmcnt(0), the whole first ring)
+    depthwise(0, 0, 0);
+
+    f32x16 acc;
+    float rv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f, rv[r] = 0.f;
+    const int mb = wm * 32;  // this wave's 32 output channels
+
+    int rs_next = 1 % R.D;  // ring slot of stage g + 1
+    for (int g = 0; g < nstages; ++g) {
+        // stage g + 1 has landed (this wave's part: the later stages may stay in flight) ...
+        if (g + 1 < nstages && !(R.dbg & 4)) wait_vmcnt((issued - (g + 2)) * cnt_w);
+        // ... for every wave; every wave is done with chunk g - 1 (its slot and tile buffers)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (issued < nstages) {  // into the slot chunk g's depthwise read (chunk g - 1's MFMAs are done)
+            issue(issued, issued % R.D);
+            ++issued;
+        }
+        const int c = g % R.nch, kc = c * FK;
+        const float *bD = sD + (g & 1) * FK * DS, *bW = sW + (size_t)kc * Mpad;
+        if (!(R.dbg & 1))
+#pragma unroll
+        for (int s = 0; s < FK / 2; ++s)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bW[(2 * s + kh) * Mpad + mb + col],
+                                                       bD[(2 * s + kh) * DS + wn * 32 + col], acc, 0, 0, 0);
+        if (R.res) {  // the chunk's residual rows of this wave's accumulator rows
+            const float *bR = sR + (g & 1) * FK * DS + wn * 32 + col;
+            if (kc == mb) {
+#pragma unroll
+                for (int r = 0; r < 8; ++r) rv[r] = bR[mfma32_row(r, kh) * DS];
+            } else if (kc == mb + 16) {
+#pragma unroll
+                for (int r = 8; r < 16; ++r) rv[r] = bR[(mfma32_row(r, kh) - 16) * DS];
+            }
+        }
+        // the next chunk's depthwise while this chunk's MFMAs drain (other tile buffers)
+        if (g + 1 < nstages) depthwise(g + 1, rs_next, (g + 1) & 1);
+        rs_next = rs_next + 1 == R.D ? 0 : rs_next + 1;
+        if (c == R.nch - 1) {  // the tile's last chunk: epilogue (bias, act, residual, act, store)
+            const int j = tile_of(g) * BN + wn * 32 + col;
+            if (j < G.ncols && !(R.dbg & 8)) {
+                const int n = j / Pq, q = j - n * Pq;
+                const uint32_t ob = (uint32_t)n * (uint32_t)G.o_sN + (uint32_t)q * (uint32_t)G.o_sP;
+                float v[16];
+                auto chan = [&](int r) { return mb + mfma32_row(r, kh); };
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v[r] = acc[r] + sB[chan(r)];
+                ring_act_n<16>(G.pre.kind, G.pre.lo, G.pre.hi, sPre, v, chan);
+                if (R.res) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) v[r] += rv[r];
+                }
+                ring_act_n<16>(G.post.kind, G.post.lo, G.post.hi, sPost, v, chan);
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (chan(r) < G.M) G.out[ob + (uint32_t)chan(r) * (uint32_t)G.o_sC] = v[r];
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.f, rv[r] = 0.f;
+        }
+    }
+}
+
+namespace {
+
+struct DwPwLayout {
+    int wm, mtw, ntw;
+    int bm() const { return wm * mtw * 32; }
+    int bn() const { return (4 / wm) * ntw * 32; }
+};
+// the instantiated layouts (BM x BN): 32x128 64x128 96x128 128x128 | 64x64 128x64 256x64 |
+// 128x32 256x32
+constexpr DwPwLayout kLayouts[] = {{1, 1, 1}, {1, 2, 1}, {1, 3, 1}, {1, 4, 1}, {2, 1, 1},
+                                   {2, 2, 1}, {2, 4, 1}, {4, 1, 1}, {4, 2, 1}};
+
+// The V4 depthwise form (see dwpw_kernel) applies when rows split into aligned quads and the
+// layer uses the models' TF-style pads.
+static bool v4_ok(const DwPwParams &p) {
+    const int pl = p.stride == 1 ? p.k / 2 : p.k / 2 - 1;
+    return form_on(FORM_V4) && p.OW % 4 == 0 && p.in.W % 4 == 0 && p.pad_l == pl && p.pad_t == pl &&
+           p.g.ncols % 4 == 0 && p.g.P % 4 == 0;
+}
+
+// LDS bytes of the DMA form for this layer and tile (0 when it does not apply): the longest
+// input run any BN-column tile needs, rounded to 16 B, and whole 1 KiB DMA wave-instructions.
+template <int K, int S, int WM, int MTW, int DFKC>
+static size_t dma_plan(const DwPwParams &p, int *runmax, int *bufsz) {
+    constexpr int BN = (4 / WM) * 32, BM = WM * MTW * 32, KKP = (DFKC * K * K + 3) / 4 * 4;
+    const int H = p.in.H, W = p.in.W, Pin = H * W, Pq = p.g.P, OW = p.OW;
+    // (runs are rounded out to 16-B ends inside the channel plane: sC % 4 == 0 leaves room)
+    if (!form_on(FORM_DMA) || p.in.sN != Pin || p.in.sC % 4 || p.g.K % 4 ||
+        ((uintptr_t)p.in.p | (uintptr_t)p.g.wt | (uintptr_t)p.dw_w | (uintptr_t)p.dw_b) % 16)
+        return 0;
+    int rm = 0;
+    for (int j0 = 0; j0 < p.g.ncols; j0 += BN) {  // tiles repeat with the image period
+        const int jb = std::min(j0 + BN, p.g.ncols) - 1;
+        const int na = j0 / Pq, qa = j0 - na * Pq, nb = jb / Pq, qb = jb - nb * Pq;
+        const int ya = std::max(qa / OW * S - p.pad_t, 0), yb = std::min(qb / OW * S - p.pad_t + K - 1, H - 1);
+        const int s0 = (na * Pin + ya * W) & ~3, e0 = (nb * Pin + (yb + 1) * W + 3) & ~3;
+        rm = std::max(rm, e0 - s0);
+        if (na >= 4 && (j0 % Pq) == 0) break;  // the pattern has repeated (whole images seen)
+    }
+    const int words = DFKC * rm + (MTW == 1 ? 0 : DFKC * BM) + KKP + DFKC;  // (WREG: no 1x1 weights)
+    *runmax = rm;
+    *bufsz = (words + 255) / 256 * 256;
+    if (p.pad_t * W + p.pad_l > 256) return 0;  // the guard in front of the buffers
+    const size_t lds = sizeof(float) * (256 + 2 * (size_t)*bufsz + DFKC * BN);
+    return lds <= 80 * 1024 ? lds : 0;
+}
+
+// the widest channel chunk the DMA form may use (ZARU_HIP_DFKC: 16 / 32 / 64, for A/B runs)
+static int dfkc_max() {
+    static const int v = [] {
+        const char *e = std::getenv("ZARU_HIP_DFKC");
+        const long x = e ? std::strtol(e, nullptr, 10) : 0;
+        return x >= 64 ? 64 : x >= 32 ? 32 : 16;
+    }();
+    return v;
+}
+
+template <int K, int S, int WM, int MTW>
+const char *dwpw_go(const DwPwParams &p, hipStream_t s) {
+    constexpr int BN = (4 / WM) * 32, BM = WM * MTW * 32;
+    const int nct = (p.g.ncols + BN - 1) / BN;
+    const int mb = (p.g.Mpad + BM - 1) / BM;
+    dim3 grid((nct + 7) / 8 * 8, mb);
+    int runmax = 0, bufsz = 0;
+    if constexpr (K == 3 && MTW == 1) {
+        // wider channel chunks: fewer dependent DMA round trips per tile (the 6^2 / 3^2 launches
+        // of a few dozen workgroups are nothing but those round trips)
+        if (dfkc_max() >= 64)
+            if (const size_t lds = dma_plan<K, S, WM, MTW, 64>(p, &runmax, &bufsz)) {
+                hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, 64>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
+                return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,64>", K, S, WM, MTW);
+            }
+        if (dfkc_max() >= 32)
+            if (const size_t lds = dma_plan<K, S, WM, MTW, 32>(p, &runmax, &bufsz)) {
+                hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, 32>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
+                return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,32>", K, S, WM, MTW);
+            }
+    }
+    if (const size_t lds = dma_plan<K, S, WM, MTW, 16>(p, &runmax, &bufsz)) {
+        hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, 16>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
+        return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,16>", K, S, WM, MTW);
+    }
+    const bool v4 = v4_ok(p);
+    if (v4) hipLaunchKernelGGL((dwpw_kernel<K, S, WM, MTW, 1, true>), grid, dim3(256), 0, s, p, nct);
+    else hipLaunchKernelGGL((dwpw_kernel<K, S, WM, MTW, 1, false>), grid, dim3(256), 0, s, p, nct);
+    return kernel_name("dwpw_kernel<%d,%d,%d,%d,1,%s>", K, S, WM, MTW, v4 ? "true" : "false");
+}
+
+template <int K, int S>
+const char *dwpw_layout(const DwPwParams &p, const DwPwLayout &l, hipStream_t s) {
+    switch (l.wm * 10 + l.mtw) {
+    case 11: return dwpw_go<K, S, 1, 1>(p, s);
+    case 12: return dwpw_go<K, S, 1, 2>(p, s);
+    case 13: return dwpw_go<K, S, 1, 3>(p, s);
+    case 14: return dwpw_go<K, S, 1, 4>(p, s);
+    case 21: return dwpw_go<K, S, 2, 1>(p, s);
+    case 22: return dwpw_go<K, S, 2, 2>(p, s);
+    case 24: return dwpw_go<K, S, 2, 4>(p, s);
+    case 41: return dwpw_go<K, S, 4, 1>(p, s);
+    default: return dwpw_go<K, S, 4, 2>(p, s);
+    }
+}
+
+// The ring form's plan for one launch, or nullptr when it does not apply: a single M tile
+// (Mpad <= 256), a CNHW input with 16-B aligned channel planes, a residual that is the block
+// input (or none), and the weights, parameters and a ring of >= 2 stages within the LDS.
+template <int K, int S, int WM>
+static const char *ring_go(const DwPwParams &p, hipStream_t s) {
+    constexpr int BN = (8 / WM) * 32, BM = WM * 32, FK = RING_DFKC, KK = K * K;
+    const GemmParams &g = p.g;
+    const int H = p.in.H, W = p.in.W, Pin = H * W, Pq = g.P, OW = p.OW, OH = g.P / p.OW;
+    if (p.in.sN != Pin || p.in.sC % 4 || ((uintptr_t)p.in.p | (uintptr_t)g.wt) % 16 || g.Mpad % 4 ||
+        g.Mpad > BM || p.pad_t * W + p.pad_l > 256)
+        return nullptr;
+    int res = 0;
+    if (g.res_mode != 0) {
+        const int PL = DwPad<K, S>::L;
+        if (g.r != p.in.p || g.r_sN != p.in.sN || g.r_sC != p.in.sC || g.r_C > g.K || p.pad_t != PL ||
+            p.pad_l != PL)
+            return nullptr;
+        if (g.res_mode == 1 && S == 1 && OW == W && OH == H) res = 1;
+        else if (g.res_mode == 2 && S == 2 && g.r_W == W && H % 2 == 0 && W % 2 == 0 && 2 * OW == W &&
+                 2 * OH == H && PL + 1 < K)
+            res = 2;
+        else
+            return nullptr;
+    }
+    RingPlan R{};
+    R.nct = (g.ncols + BN - 1) / BN;
+    R.nch = (g.K + FK - 1) / FK;
+    int rm = 0;
+    for (int j0 = 0; j0 < g.ncols; j0 += BN) {  // tiles repeat with the image period
+        const int jb = std::min(j0 + BN, g.ncols) - 1;
+        const int na = j0 / Pq, qa = j0 - na * Pq, nb = jb / Pq, qb = jb - nb * Pq;
+        const int ya = std::max(qa / OW * S - p.pad_t, 0), yb = std::min(qb / OW * S - p.pad_t + K - 1, H - 1);
+        const int s0 = (na * Pin + ya * W) & ~3, e0 = (nb * Pin + (yb + 1) * W + 3) & ~3;
+        rm = std::max(rm, e0 - s0);
+        if (na >= 4 && (j0 % Pq) == 0) break;
+    }
+    R.rq = rm / 4;
+    R.stg = (FK * R.rq + 63) / 64 * 256;
+    R.res = res;
+    static const int dbg = [] { const char *e = std::getenv("ZARU_HIP_DBG"); return e ? (int)std::strtol(e, nullptr, 10) : 0; }();
+    R.dbg = dbg;
+    const int kr = R.nch * FK, bm = std::max(g.Mpad, BM);
+    // fixed part (floats): guard, weights, depthwise weights / biases / slopes, bias and slopes,
+    // two depthwise tiles (+ two residual tiles)
+    const int fixed = 256 + kr * g.Mpad + (kr * KK + 3) / 4 * 4 + 2 * kr + 3 * bm + 2 * FK * BN * (res ? 2 : 1);
+    const int budget = 160 * 1024 / 4;
+    const int D = std::min(8, (budget - fixed) / R.stg);
+    if (D < 2) return nullptr;
+    R.D = D;
+    R.o_ring = 256;
+    R.o_w = R.o_ring + D * R.stg;
+    R.o_dw = R.o_w + kr * g.Mpad;
+    R.o_db = R.o_dw + (kr * KK + 3) / 4 * 4;
+    R.o_sdw = R.o_db + kr;
+    R.o_b = R.o_sdw + kr;
+    R.o_spre = R.o_b + bm;
+    R.o_spost = R.o_spre + bm;
+    R.o_d = R.o_spost + bm;
+    R.o_r = R.o_d + 2 * FK * BN;
+    R.lds_floats = R.o_r + (res ? 2 * FK * BN : 0);
+    static const int ncu = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return n;
+    }();
+    const int G = (std::min(R.nct, ncu) + 7) / 8 * 8;
+    R.tpx = (R.nct + 7) / 8;
+    static const bool attr = [] {
+        return hipFuncSetAttribute((const void *)dwpw_ring_kernel<K, S, WM>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    }();
+    (void)attr;
+    hipLaunchKernelGGL((dwpw_ring_kernel<K, S, WM>), dim3(G), dim3(512), sizeof(float) * (size_t)R.lds_floats, s, p, R);
+    return kernel_name("dwpw_ring_kernel<%d,%d,%d>", K, S, WM);
+}
+
+template <int K, int S>
+static const char *ring_launch(const DwPwParams &p, hipStream_t s) {
+    if (p.g.Mpad <= 64) return ring_go<K, S, 2>(p, s);
+    if (p.g.Mpad <= 128) return ring_go<K, S, 4>(p, s);
+    return ring_go<K, S, 8>(p, s);
+}
+
+}  // namespace
+
+// Layout choice for the MFMA forms: no M split unless Mpad > 256, at most 1/3 padded rows;
+// among those, the widest column tile that still gives >= 4 workgroups per CU (else the most
+// workgroups).
+const char *launch_dwpw_mfma(const DwPwParams &p, hipStream_t s) {
+    if (form_on(FORM_RING) && p.g.Mpad <= 256) {
+        const char *k = p.k == 3 ? (p.stride == 1 ? ring_launch<3, 1>(p, s) : ring_launch<3, 2>(p, s))
+                                 : (p.stride == 1 ? ring_launch<5, 1>(p, s) : ring_launch<5, 2>(p, s));
+        if (k) return k;
+    }
+    // workgroups one launch should reach (ZARU_HIP_MINWGS overrides it for layout sweeps)
+    static const int64_t min_wgs = [] {
+        const char *e = std::getenv("ZARU_HIP_MINWGS");
+        const long v = e ? std::strtol(e, nullptr, 10) : 0;
+        return (int64_t)(v > 0 ? v : 1024);
+    }();
+    const DwPwLayout *best = nullptr;
+    int64_t best_wgs = 0;
+    for (const DwPwLayout &l : kLayouts) {
+        const int mb = (p.g.Mpad + l.bm() - 1) / l.bm();
+        if (mb > 1 && l.bm() < 256) continue;
+        if ((int64_t)mb * l.bm() * 3 > (int64_t)p.g.Mpad * 4 && p.g.Mpad <= 256) continue;
+        const int64_t wgs = (int64_t)((p.g.ncols + l.bn() - 1) / l.bn()) * mb;
+        bool better;
+        if (!best) better = true;
+        else if ((wgs >= min_wgs) != (best_wgs >= min_wgs)) better = wgs >= min_wgs;
+        else if (wgs >= min_wgs) better = l.bn() > best->bn() || (l.bn() == best->bn() && l.bm() < best->bm());
+        else better = wgs > best_wgs || (wgs == best_wgs && l.bm() < best->bm());
+        if (better) {
+            best = &l;
+            best_wgs = wgs;
+        }
+    }
+    if (!best) {
+        // no tile height wastes <= 1/3 of its rows without an M split (e.g. Mpad = 160, the
+        // 144-channel blocks of BlazeFace full range): the unsplit tile with the fewest padded
+        // rows, else the tallest split one
+        int waste = 1 << 30;
+        for (const DwPwLayout &l : kLayouts) {
+            const int mb = (p.g.Mpad + l.bm() - 1) / l.bm();
+            if (mb > 1 && l.bm() < 256) continue;
+            const int w = mb * l.bm() - p.g.Mpad;
+            if (w < waste) {
+                waste = w;
+                best = &l;
+            }
+        }
+    }
+    if (p.k == 3) return p.stride == 1 ? dwpw_layout<3, 1>(p, *best, s) : dwpw_layout<3, 2>(p, *best, s);
+    return p.stride == 1 ? dwpw_layout<5, 1>(p, *best, s) : dwpw_layout<5, 2>(p, *best, s);
+}
+
+
+}  // namespace zr

@@ -238,13 +238,14 @@ struct ChainParams {
 
 // Kernel forms the launchers and the plan compiler choose between.  Every form computes the same
 // arithmetic in the same order, so switching one changes no output bit (tests/test_gpu_forms.py).
-// ZARU_HIP_FORMS, read once per process, switches forms off ("-dma,-v4") or the opt-in chain form
-// on ("+chain"), for verification and A/B runs.
+// ZARU_HIP_FORMS, read once per process, switches forms off ("-dma,-v4") or the opt-in chain / ring
+// forms on ("+chain", "+ring"), for verification and A/B runs.
 //   dma: LDS-DMA staged MFMA dwpw (dwpw_dma_kernel)   v4: windowed depthwise taps (dwpw_kernel)
 //   valu: VALU dwpw for few-channel high-resolution layers   valu_db: its double-buffered staging
 //   rows: image-row head GEMM (gemm_rows_kernel)   chain: low-resolution layer runs (chain.hip)
 //   vres: VALU dwpw taking the block's residual from the staged depthwise taps
-enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_CHAIN, FORM_VRES, FORM_VSTORE, FORM_COUNT };
+//   vstore: 16-B row-segment GEMM epilogue   ring: persistent LDS-ring MFMA dwpw (dwpw_mfma.hip)
+enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_CHAIN, FORM_VRES, FORM_VSTORE, FORM_RING, FORM_COUNT };
 bool form_on(Form f);
 
 bool stem_supported(int cin, int k, int stride, int cout);
@@ -266,6 +267,7 @@ const char *launch_preproc(const PreprocParams &p, hipStream_t s);
 const char *launch_candidates(const CandParams &p, hipStream_t s);
 const char *launch_stem(const StemParams &p, bool pre, hipStream_t s);
 const char *launch_dwpw(const DwPwParams &p, hipStream_t s);
+const char *launch_dwpw_mfma(const DwPwParams &p, hipStream_t s);  // the MFMA forms (dwpw_mfma.hip)
 const char *launch_chain(const ChainParams &p, hipStream_t s);
 
 }  // namespace zr
