@@ -498,12 +498,11 @@ struct RingPlan {
     int res;          // residual from the staged taps: 0 none, 1 centre tap, 2 2x2 max-pool
     // LDS offsets (floats)
     int o_ring, o_w, o_dw, o_db, o_b, o_spre, o_spost, o_sdw, o_d, o_r, lds_floats;
-    int dbg;
 };
 
-template <int K, int S, int WM>
+template <int K, int S, int WM, bool RES>
 __global__ __launch_bounds__(512) void dwpw_ring_kernel(const DwPwParams P, const RingPlan R) {
-    constexpr int NW = 8, WN = NW / WM, BN = WN * 32, BM = WM * 32, KK = K * K, FK = RING_DFKC;
+    constexpr int NW = 8, WN = NW / WM, BN = WN * 32, KK = K * K, FK = RING_DFKC;
     constexpr int CPAR = 512 / BN, PER = FK / CPAR;
     constexpr int PL = DwPad<K, S>::L;  // the residual taps (the host checks the pads are these)
     static_assert(PER >= 1 && FK % CPAR == 0, "tile / chunk mismatch");
@@ -521,18 +520,19 @@ __global__ __launch_bounds__(512) void dwpw_ring_kernel(const DwPwParams P, cons
     if (ntl == 0) return;  // whole workgroup, before any barrier
     const int nstages = ntl * R.nch;
     const int Cin = G.K, H = P.in.H, W = P.in.W, Pin = H * W, OW = P.OW, Pq = G.P;
-    const int pt = P.pad_t, pl = P.pad_l, Mpad = G.Mpad;
+    const int pt = P.pad_t, pl = P.pad_l, Mpad = G.Mpad, rs4 = R.rq * 4;
+    const float inv_pq = 1.f / (float)Pq, inv_ow = 1.f / (float)OW, inv_rq = 1.f / (float)R.rq;
     float *ring = lds + R.o_ring, *sW = lds + R.o_w, *sDW = lds + R.o_dw, *sDB = lds + R.o_db;
     float *sB = lds + R.o_b, *sPre = lds + R.o_spre, *sPost = lds + R.o_spost, *sDS = lds + R.o_sdw;
     float *sD = lds + R.o_d, *sR = lds + R.o_r;
     constexpr int DS = BN;  // depthwise-tile row stride
 
     // ---- once per workgroup: weights, depthwise parameters, bias and slopes into LDS
-    if (!(R.dbg & 16)) {
+    {
         const int kr = R.nch * FK;  // weight rows staged (rows >= Kpad are zero)
-        const int n4 = kr * Mpad / 4;
+        const int m4 = Mpad / 4, n4 = kr * m4;
         for (int i = tid; i < n4; i += 512) {
-            const int k = (4 * i) / Mpad, m = 4 * i - k * Mpad;
+            const int k = i / m4, m = 4 * (i - k * m4);
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
             if (k < G.Kpad) v = *reinterpret_cast<const float4 *>(G.wt + (size_t)k * Mpad + m);
             *reinterpret_cast<float4 *>(sW + 4 * i) = v;
@@ -549,53 +549,59 @@ __global__ __launch_bounds__(512) void dwpw_ring_kernel(const DwPwParams P, cons
         }
     }
 
-    // ---- the DMA of stage q (tile t_beg + (q / nch) * G8, chunk q % nch) into ring slot
-    const int nwi = R.stg >> 8;                                      // wave-instructions per stage
-    const int cnt_w = wave < nwi ? (nwi - wave + NW - 1) / NW : 0;  // of them issued by this wave
-    const float inv_rq = 1.f / (float)R.rq;
-    auto tile_of = [&](int q) { return t_beg + (q / R.nch) * G8; };
+    // the input run of tile t: first float (16-B aligned, from a channel's base) and length / 4
     auto run_of = [&](int t, int &s0, int &run4) {
         const int ja = t * BN, jb = min(ja + BN, G.ncols) - 1;
-        const int na = ja / Pq, qa = ja - na * Pq, nb = jb / Pq, qb = jb - nb * Pq;
-        const int ya = max(qa / OW * S - pt, 0), yb = min(qb / OW * S - pt + K - 1, H - 1);
+        const int na = qdiv(ja, Pq, inv_pq), qa = ja - na * Pq, nb = qdiv(jb, Pq, inv_pq), qb = jb - nb * Pq;
+        const int ya = max(qdiv(qa, OW, inv_ow) * S - pt, 0), yb = min(qdiv(qb, OW, inv_ow) * S - pt + K - 1, H - 1);
         s0 = (na * Pin + ya * W) & ~3;
         run4 = (((nb * Pin + (yb + 1) * W + 3) & ~3) - s0) >> 2;
     };
-    auto issue = [&](int q, int rs) {
-        const int t = tile_of(q), kc = (q % R.nch) * FK;
-        int s0, run4;
-        run_of(t, s0, run4);
-        float *dst = ring + rs * R.stg;
-        if (R.dbg & 4) return;
+
+    // ---- the DMA side: stages in (tile, chunk) order, D - 1 ahead of the compute side
+    const int nwi = R.stg >> 8;                                      // wave-instructions per stage
+    const int cnt_w = wave < nwi ? (nwi - wave + NW - 1) / NW : 0;  // of them issued by this wave
+    int i_tile = t_beg, i_chunk = 0, i_s0 = 0, i_run4 = 0, i_slot = 0, issued = 0;
+    run_of(i_tile, i_s0, i_run4);
+    auto issue_next = [&]() {
+        const int kc = i_chunk * FK;
+        float *dst = ring + i_slot * R.stg;
         for (int wi = wave; wi < nwi; wi += NW) {
             const int sl = wi * 64 + lane;
             const int c = qdiv(sl, R.rq, inv_rq), i = sl - c * R.rq;
             const float *src = (const float *)&zr_zero4;
-            if (c < FK && kc + c < Cin && i < run4)
-                src = P.in.p + (size_t)(uint32_t)(kc + c) * (uint32_t)P.in.sC + (uint32_t)(s0 + 4 * i);
+            if (c < FK && kc + c < Cin && i < i_run4)
+                src = P.in.p + (size_t)(uint32_t)(kc + c) * (uint32_t)P.in.sC + (uint32_t)(i_s0 + 4 * i);
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
                                              (__attribute__((address_space(3))) void *)(dst + wi * 256), 16, 0, 0);
         }
+        ++issued;
+        i_slot = i_slot + 1 == R.D ? 0 : i_slot + 1;
+        if (++i_chunk == R.nch) {
+            i_chunk = 0;
+            i_tile += G8;
+            if (i_tile < t_end) run_of(i_tile, i_s0, i_run4);
+        }
     };
 
-    // ---- depthwise role: column dj of the tile, channels dc + CPAR * i of each chunk
+    // ---- the depthwise side (stage g + 1 while the MFMAs take stage g): column dj of the tile,
+    // channels dc + CPAR * i of each chunk
     const int dj = tid % BN;
     int dc = tid / BN;
     if constexpr (BN >= 64) dc = __builtin_amdgcn_readfirstlane(dc);  // one channel per wave
-    int d_tile = -1, d_s0 = 0, d_tb = 0;
+    int d_tile = t_beg - G8, d_chunk = R.nch - 1, d_slot = 0, d_tb = 0;
     uint32_t d_mask = 0;
-    // chunk of stage q: depthwise (+ residual taps) from its ring slot into tile buffer db
-    auto depthwise = [&](int q, int rs, int db) {
-        const int t = tile_of(q), kc = (q % R.nch) * FK;
-        if (t != d_tile) {  // per-tile geometry of this thread's column
-            d_tile = t;
-            int run4;
-            run_of(t, d_s0, run4);
-            const int jd = min(t * BN + dj, G.ncols - 1);
-            const int n = jd / Pq, qq = jd - n * Pq;
-            const int oy = qq / OW, ox = qq - oy * OW;
+    auto d_advance = [&]() {  // to the next stage; a new tile's per-thread tap geometry
+        if (++d_chunk == R.nch) {
+            d_chunk = 0;
+            d_tile += G8;
+            int s0, run4;
+            run_of(d_tile, s0, run4);
+            const int jd = min(d_tile * BN + dj, G.ncols - 1);
+            const int n = qdiv(jd, Pq, inv_pq), qq = jd - n * Pq;
+            const int oy = qdiv(qq, OW, inv_ow), ox = qq - oy * OW;
             const int iy0 = oy * S - pt, ix0 = ox * S - pl;
-            d_tb = n * Pin + iy0 * W + ix0 - d_s0;
+            d_tb = n * Pin + iy0 * W + ix0 - s0;
             d_mask = 0;
 #pragma unroll
             for (int ky = 0; ky < K; ++ky)
@@ -605,17 +611,19 @@ __global__ __launch_bounds__(512) void dwpw_ring_kernel(const DwPwParams P, cons
                     d_mask |= (iy >= 0 && iy < H && ix >= 0 && ix < W ? 1u : 0u) << (ky * K + kx);
                 }
         }
-        const float *stage = ring + rs * R.stg;
-        if (R.dbg & 2) return;
-        float x[PER][KK];
+    };
+    float x[PER][KK];
+    auto d_load = [&]() {  // this thread's taps of the current depthwise stage
+        const float *stage = ring + d_slot * R.stg + d_tb;
 #pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const float *t0 = stage + (dc + CPAR * i) * (R.rq * 4) + d_tb;
+        for (int i = 0; i < PER; ++i)
 #pragma unroll
             for (int ky = 0; ky < K; ++ky)
 #pragma unroll
-                for (int kx = 0; kx < K; ++kx) x[i][ky * K + kx] = t0[ky * W + kx];
-        }
+                for (int kx = 0; kx < K; ++kx) x[i][ky * K + kx] = stage[(dc + CPAR * i) * rs4 + ky * W + kx];
+    };
+    auto d_compute = [&](int db) {  // depthwise (+ residual taps) of the loaded taps into tile db
+        const int kc = d_chunk * FK;
         float dv[PER];
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
@@ -634,7 +642,7 @@ __global__ __launch_bounds__(512) void dwpw_ring_kernel(const DwPwParams P, cons
         for (int i = 0; i < PER; ++i) {
             const int c = kc + dc + CPAR * i;
             sD[db * FK * DS + (dc + CPAR * i) * DS + dj] = c < Cin ? dv[i] : 0.f;
-            if (R.res) {
+            if constexpr (RES) {
                 float r;
                 if constexpr (S == 1) {
                     r = x[i][PL * K + PL];
@@ -645,38 +653,54 @@ __global__ __launch_bounds__(512) void dwpw_ring_kernel(const DwPwParams P, cons
                 sR[db * FK * DS + (dc + CPAR * i) * DS + dj] = c < G.r_C ? r : 0.f;
             }
         }
+        d_slot = d_slot + 1 == R.D ? 0 : d_slot + 1;
     };
 
     // ---- prologue: parameters visible, first D stages in flight, chunk 0's depthwise
-    int issued = min(R.D, nstages);
-    for (int q = 0; q < issued; ++q) issue(q, q);
+    while (issued < R.D && issued < nstages) issue_next();
     __syncthreads();  // the parameter stores (and, through vmcnt(0), the whole first ring)
-    depthwise(0, 0, 0);
+    d_advance();
+    d_load();
+    d_compute(0);
 
     f32x16 acc;
     float rv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f, rv[r] = 0.f;
     const int mb = wm * 32;  // this wave's 32 output channels
+    int c_tile = t_beg, c_chunk = 0;
 
-    int rs_next = 1 % R.D;  // ring slot of stage g + 1
     for (int g = 0; g < nstages; ++g) {
+        const bool more = g + 1 < nstages;
         // stage g + 1 has landed (this wave's part: the later stages may stay in flight) ...
-        if (g + 1 < nstages && !(R.dbg & 4)) wait_vmcnt((issued - (g + 2)) * cnt_w);
+        if (more) wait_vmcnt((issued - (g + 2)) * cnt_w);
         // ... for every wave; every wave is done with chunk g - 1 (its slot and tile buffers)
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (issued < nstages) {  // into the slot chunk g's depthwise read (chunk g - 1's MFMAs are done)
-            issue(issued, issued % R.D);
-            ++issued;
-        }
-        const int c = g % R.nch, kc = c * FK;
-        const float *bD = sD + (g & 1) * FK * DS, *bW = sW + (size_t)kc * Mpad;
-        if (!(R.dbg & 1))
+        if (issued < nstages) issue_next();  // into the slot chunk g's depthwise read
+        if (more) d_advance();
+
+        // chunk g's MFMAs interleaved with chunk g + 1's depthwise (independent tile buffers)
+        const int kc = c_chunk * FK;
+        const float *bD = sD + (g & 1) * FK * DS + wn * 32 + col, *bW = sW + (size_t)kc * Mpad + mb + col;
+        float av[FK / 2], bv[FK / 2];
 #pragma unroll
-        for (int s = 0; s < FK / 2; ++s)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bW[(2 * s + kh) * Mpad + mb + col],
-                                                       bD[(2 * s + kh) * DS + wn * 32 + col], acc, 0, 0, 0);
-        if (R.res) {  // the chunk's residual rows of this wave's accumulator rows
+        for (int s = 0; s < FK / 2; ++s) {
+            av[s] = bW[(2 * s + kh) * Mpad];
+            bv[s] = bD[(2 * s + kh) * DS];
+        }
+        // (after the last chunk this recomputes a stale stage into the idle tile buffer: no
+        // branch, so the scheduler can interleave the two instruction streams)
+        d_load();
+#pragma unroll
+        for (int s = 0; s < FK / 2; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
+        d_compute((g + 1) & 1);
+#pragma unroll
+        for (int s = 0; s < FK / 2; ++s) {  // 1 MFMA, then a share of the depthwise VALU / LDS work
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2 + PER * KK / (FK / 2), 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2 + (PER * KK * 2) / (FK / 2), 0);
+        }
+        if constexpr (RES) {  // the chunk's residual rows of this wave's accumulator rows
             const float *bR = sR + (g & 1) * FK * DS + wn * 32 + col;
             if (kc == mb) {
 #pragma unroll
@@ -686,20 +710,19 @@ __global__ __launch_bounds__(512) void dwpw_ring_kernel(const DwPwParams P, cons
                 for (int r = 8; r < 16; ++r) rv[r] = bR[(mfma32_row(r, kh) - 16) * DS];
             }
         }
-        // the next chunk's depthwise while this chunk's MFMAs drain (other tile buffers)
-        if (g + 1 < nstages) depthwise(g + 1, rs_next, (g + 1) & 1);
-        rs_next = rs_next + 1 == R.D ? 0 : rs_next + 1;
-        if (c == R.nch - 1) {  // the tile's last chunk: epilogue (bias, act, residual, act, store)
-            const int j = tile_of(g) * BN + wn * 32 + col;
-            if (j < G.ncols && !(R.dbg & 8)) {
-                const int n = j / Pq, q = j - n * Pq;
+        if (++c_chunk == R.nch) {  // the tile's last chunk: epilogue (bias, act, residual, act, store)
+            c_chunk = 0;
+            const int j = c_tile * BN + wn * 32 + col;
+            c_tile += G8;
+            if (j < G.ncols) {
+                const int n = qdiv(j, Pq, inv_pq), q = j - n * Pq;
                 const uint32_t ob = (uint32_t)n * (uint32_t)G.o_sN + (uint32_t)q * (uint32_t)G.o_sP;
                 float v[16];
                 auto chan = [&](int r) { return mb + mfma32_row(r, kh); };
 #pragma unroll
                 for (int r = 0; r < 16; ++r) v[r] = acc[r] + sB[chan(r)];
                 ring_act_n<16>(G.pre.kind, G.pre.lo, G.pre.hi, sPre, v, chan);
-                if (R.res) {
+                if constexpr (RES) {
 #pragma unroll
                     for (int r = 0; r < 16; ++r) v[r] += rv[r];
                 }
@@ -856,8 +879,6 @@ static const char *ring_go(const DwPwParams &p, hipStream_t s) {
     R.rq = rm / 4;
     R.stg = (FK * R.rq + 63) / 64 * 256;
     R.res = res;
-    static const int dbg = [] { const char *e = std::getenv("ZARU_HIP_DBG"); return e ? (int)std::strtol(e, nullptr, 10) : 0; }();
-    R.dbg = dbg;
     const int kr = R.nch * FK, bm = std::max(g.Mpad, BM);
     // fixed part (floats): guard, weights, depthwise weights / biases / slopes, bias and slopes,
     // two depthwise tiles (+ two residual tiles)
@@ -886,12 +907,16 @@ static const char *ring_go(const DwPwParams &p, hipStream_t s) {
     const int G = (std::min(R.nct, ncu) + 7) / 8 * 8;
     R.tpx = (R.nct + 7) / 8;
     static const bool attr = [] {
-        return hipFuncSetAttribute((const void *)dwpw_ring_kernel<K, S, WM>,
+        return hipFuncSetAttribute((const void *)dwpw_ring_kernel<K, S, WM, false>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess &&
+               hipFuncSetAttribute((const void *)dwpw_ring_kernel<K, S, WM, true>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
     }();
     (void)attr;
-    hipLaunchKernelGGL((dwpw_ring_kernel<K, S, WM>), dim3(G), dim3(512), sizeof(float) * (size_t)R.lds_floats, s, p, R);
-    return kernel_name("dwpw_ring_kernel<%d,%d,%d>", K, S, WM);
+    const size_t lds = sizeof(float) * (size_t)R.lds_floats;
+    if (res) hipLaunchKernelGGL((dwpw_ring_kernel<K, S, WM, true>), dim3(G), dim3(512), lds, s, p, R);
+    else hipLaunchKernelGGL((dwpw_ring_kernel<K, S, WM, false>), dim3(G), dim3(512), lds, s, p, R);
+    return kernel_name("dwpw_ring_kernel<%d,%d,%d,%s>", K, S, WM, res ? "true" : "false");
 }
 
 template <int K, int S>

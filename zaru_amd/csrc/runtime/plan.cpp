@@ -83,6 +83,7 @@ class Compiler {
     bool act_from_node(const OnnxNode &nd, int C, int Cpad, ActDesc &a);
     void finalize_outputs();
     void allocate();
+    void mark_inverted_residuals();
     void schedule_sinks();
     void form_chains();
 };
@@ -852,6 +853,25 @@ bool Compiler::lower() {
     return true;
 }
 
+// Expand 1x1 -> (depthwise -> 1x1) pairs whose expanded tensor nothing else reads: run_plan may
+// launch them as one inverted-residual kernel (ir.hip), the expanded tensor never stored.
+void Compiler::mark_inverted_residuals() {
+    std::vector<int> reads(P.storage_size.size(), 0);
+    for (const Step &s : P.steps) {
+        for (const TRef *r : {&s.in, &s.in2})
+            if (r->kind == 0 && r->id >= 0) reads[r->id]++;
+        for (const TRef &r : s.chain_outs)
+            if (r.kind == 0 && r.id >= 0) reads[r.id]++;
+    }
+    for (size_t i = 0; i + 1 < P.steps.size(); i++) {
+        Step &e = P.steps[i];
+        const Step &d = P.steps[i + 1];
+        e.ir_next = e.kind == S_GEMM && e.KK == 1 && e.res_mode == 0 && e.out.kind == 0 && e.out.c_off == 0 &&
+                    e.in.kind == 0 && e.in.c_off == 0 && d.kind == S_DWPW && d.in.kind == 0 &&
+                    d.in.id == e.out.id && d.in.c_off == 0 && reads[e.out.id] == 1 && e.M == d.K;
+    }
+}
+
 void Compiler::allocate() {
     // liveness over step indices
     const size_t ns = P.storage_size.size();
@@ -865,6 +885,14 @@ void Compiler::allocate() {
                 first[r->id] = std::min(first[r->id], (int)i);
                 last[r->id] = std::max(last[r->id], (int)i);
             }
+    }
+    // a fused inverted residual (ir_next) reads the expand's input and writes the projection in
+    // ONE launch: the two must not share memory, so each is live across both steps
+    for (size_t i = 0; i + 1 < P.steps.size(); i++) {
+        if (!P.steps[i].ir_next) continue;
+        const TRef &x = P.steps[i].in, &o = P.steps[i + 1].out;
+        if (x.kind == 0 && x.id >= 0) last[x.id] = std::max(last[x.id], (int)i + 1);
+        if (o.kind == 0 && o.id >= 0) first[o.id] = std::min(first[o.id], (int)i);
     }
     std::vector<int> order(ns);
     for (size_t i = 0; i < ns; i++) order[i] = (int)i;
@@ -1268,6 +1296,7 @@ bool Compiler::run(const std::vector<uint32_t> &sel) {
                 reader = (int)i;
             }
     P.input_fusable = readers == 1 && P.steps[reader].kind == S_DIRECT && P.steps[reader].stem;
+    mark_inverted_residuals();
     allocate();
     return true;
 }
@@ -1335,87 +1364,109 @@ Plane plane_of(const TRef &r, const Plan &plan, const Binding &b) {
 
 void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook *hook) {
     const float *W = b.weights;
-    for (const Step &s : plan.steps) {
+    auto gemm_of = [&](const Step &s) {
+        Resolved out = resolve(s.out, plan, b);
+        Resolved x = resolve(s.in, plan, b);
+        GemmParams g{};
+        g.x = x.p;
+        g.x_sN = x.sN;
+        g.x_sC = x.sC;
+        g.KK = s.KK;
+        g.x_sK = 1;
+        g.pk = s.kw;
+        g.ph = s.kh;
+        g.x_W = s.in.W;
+        g.P = s.out.H * s.out.W;
+        g.ncols = b.N * g.P;
+        g.M = s.M;
+        g.K = s.K;
+        g.Mpad = s.Mpad;
+        g.Kpad = s.Kpad;
+        g.wt = W + s.w_off;
+        g.bias = W + s.b_off;
+        g.pre = act_of(s.pre, W);
+        g.post = act_of(s.post, W);
+        g.res_mode = s.res_mode;
+        if (s.res_mode) {
+            Resolved r = resolve(s.in2, plan, b);
+            g.r = r.p;
+            g.r_sN = r.sN;
+            g.r_sC = r.sC;
+            g.r_C = s.r_C;
+            g.r_W = s.in2.W;
+        }
+        g.out_W = s.out.W;
+        g.out = const_cast<float *>(out.p);
+        g.o_sN = out.sN;
+        g.o_sC = out.sC;
+        g.o_sP = out.sP;
+        return g;
+    };
+    auto dwpw_of = [&](const Step &s) {
+        Resolved out = resolve(s.out, plan, b);
+        DwPwParams d{};
+        GemmParams &g = d.g;
+        g.P = s.out.H * s.out.W;
+        g.ncols = b.N * g.P;
+        g.M = s.M;
+        g.K = s.K;
+        g.KK = 1;
+        g.Mpad = s.Mpad;
+        g.Kpad = s.Kpad;
+        g.wt = W + s.w_off;
+        g.bias = W + s.b_off;
+        g.pre = act_of(s.pre, W);
+        g.post = act_of(s.post, W);
+        g.res_mode = s.res_mode;
+        if (s.res_mode) {
+            Resolved r = resolve(s.in2, plan, b);
+            g.r = r.p;
+            g.r_sN = r.sN;
+            g.r_sC = r.sC;
+            g.r_C = s.r_C;
+            g.r_W = s.in2.W;
+        }
+        g.out_W = s.out.W;
+        g.out = const_cast<float *>(out.p);
+        g.o_sN = out.sN;
+        g.o_sC = out.sC;
+        g.o_sP = out.sP;
+        d.in = plane_of(s.in, plan, b);
+        d.OW = s.out.W;
+        d.k = s.kh;
+        d.stride = s.stride;
+        d.pad_t = s.pad_t;
+        d.pad_l = s.pad_l;
+        d.dw_w = W + s.dw_w_off;
+        d.dw_b = W + s.dw_b_off;
+        d.dw_act = act_of(s.dw_act, W);
+        return d;
+    };
+    for (size_t si = 0; si < plan.steps.size(); ++si) {
+        const Step &s = plan.steps[si];
         Resolved out = resolve(s.out, plan, b);
         const char *kname = nullptr;
         if (hook) hook->before(stream);
         switch (s.kind) {
         case S_GEMM: {
-            Resolved x = resolve(s.in, plan, b);
-            GemmParams g{};
-            g.x = x.p;
-            g.x_sN = x.sN;
-            g.x_sC = x.sC;
-            g.KK = s.KK;
-            g.x_sK = 1;
-            g.pk = s.kw;
-            g.ph = s.kh;
-            g.x_W = s.in.W;
-            g.P = s.out.H * s.out.W;
-            g.ncols = b.N * g.P;
-            g.M = s.M;
-            g.K = s.K;
-            g.Mpad = s.Mpad;
-            g.Kpad = s.Kpad;
-            g.wt = W + s.w_off;
-            g.bias = W + s.b_off;
-            g.pre = act_of(s.pre, W);
-            g.post = act_of(s.post, W);
-            g.res_mode = s.res_mode;
-            if (s.res_mode) {
-                Resolved r = resolve(s.in2, plan, b);
-                g.r = r.p;
-                g.r_sN = r.sN;
-                g.r_sC = r.sC;
-                g.r_C = s.r_C;
-                g.r_W = s.in2.W;
+            const GemmParams g = gemm_of(s);
+            if (s.ir_next && si + 1 < plan.steps.size()) {  // expand + depthwise + project, one launch
+                IrParams ir{};
+                ir.e = g;
+                ir.d = dwpw_of(plan.steps[si + 1]);
+                if (const char *k = launch_ir(ir, stream)) {
+                    const Step &n = plan.steps[si + 1];
+                    if (hook) hook->after(stream, k, (s.bytes + n.bytes - 8.0 * s.M * s.out.H * s.out.W) * b.N,
+                                          (s.flops + n.flops) * b.N);
+                    ++si;
+                    continue;
+                }
             }
-            g.out_W = s.out.W;
-            g.out = const_cast<float *>(out.p);
-            g.o_sN = out.sN;
-            g.o_sC = out.sC;
-            g.o_sP = out.sP;
             kname = launch_gemm(g, stream);
             break;
         }
         case S_DWPW: {
-            DwPwParams d{};
-            GemmParams &g = d.g;
-            g.P = s.out.H * s.out.W;
-            g.ncols = b.N * g.P;
-            g.M = s.M;
-            g.K = s.K;
-            g.KK = 1;
-            g.Mpad = s.Mpad;
-            g.Kpad = s.Kpad;
-            g.wt = W + s.w_off;
-            g.bias = W + s.b_off;
-            g.pre = act_of(s.pre, W);
-            g.post = act_of(s.post, W);
-            g.res_mode = s.res_mode;
-            if (s.res_mode) {
-                Resolved r = resolve(s.in2, plan, b);
-                g.r = r.p;
-                g.r_sN = r.sN;
-                g.r_sC = r.sC;
-                g.r_C = s.r_C;
-                g.r_W = s.in2.W;
-            }
-            g.out_W = s.out.W;
-            g.out = const_cast<float *>(out.p);
-            g.o_sN = out.sN;
-            g.o_sC = out.sC;
-            g.o_sP = out.sP;
-            d.in = plane_of(s.in, plan, b);
-            d.OW = s.out.W;
-            d.k = s.kh;
-            d.stride = s.stride;
-            d.pad_t = s.pad_t;
-            d.pad_l = s.pad_l;
-            d.dw_w = W + s.dw_w_off;
-            d.dw_b = W + s.dw_b_off;
-            d.dw_act = act_of(s.dw_act, W);
-            kname = launch_dwpw(d, stream);
+            kname = launch_dwpw(dwpw_of(s), stream);
             break;
         }
         case S_DW: {

@@ -52,6 +52,9 @@ struct Step {
     ActDesc dw_act;
     // S_DIRECT: runs as stem_kernel (Cin = 3, weights padded to 32 output channels)
     bool stem = false;
+    // S_GEMM: a plain 1x1 expand whose output only the next step (an S_DWPW) reads -- the pair
+    // may run as one inverted-residual launch (ir.hip); run_plan falls back to two launches
+    bool ir_next = false;
     // S_CHAIN: a run of layers fused into one launch (chain.hip).  `in` is the entry tensor;
     // the op table (ChainOp words) sits in the weight buffer at chain_ops_off; chain_outs are
     // the global destinations the ops' `gout` index (exports of internal tensors, graph outputs)

@@ -178,6 +178,15 @@ struct DwPwParams {
     Act dw_act;
 };
 
+// MobileNetV2 inverted residual (ir.hip): the expand 1x1 conv `e` (x = block input) feeding the
+// depthwise -> 1x1 projection `d` (d.in describes the expanded plane: C = e.M, the input's H x W),
+// in one launch; th x tw output tiles (host-chosen by launch_ir).
+struct IrParams {
+    GemmParams e;
+    DwPwParams d;
+    int th, tw, tiles_x, tiles_y;
+};
+
 // ---------------------------------------------------------------- layer chains (chain.hip)
 // A run of consecutive low-resolution layers (depthwise 3x3 -> 1x1 BlazeBlocks and plain 1x1
 // convs, <= 256 positions and <= 128 channels per image) executed by ONE workgroup per image
@@ -245,7 +254,8 @@ struct ChainParams {
 //   rows: image-row head GEMM (gemm_rows_kernel)   chain: low-resolution layer runs (chain.hip)
 //   vres: VALU dwpw taking the block's residual from the staged depthwise taps
 //   vstore: 16-B row-segment GEMM epilogue   ring: persistent LDS-ring MFMA dwpw (dwpw_mfma.hip)
-enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_CHAIN, FORM_VRES, FORM_VSTORE, FORM_RING, FORM_COUNT };
+//   ir: expand 1x1 + depthwise + project 1x1 (inverted residual) in one launch (ir.hip)
+enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_CHAIN, FORM_VRES, FORM_VSTORE, FORM_RING, FORM_IR, FORM_COUNT };
 bool form_on(Form f);
 
 bool stem_supported(int cin, int k, int stride, int cout);
@@ -268,6 +278,7 @@ const char *launch_candidates(const CandParams &p, hipStream_t s);
 const char *launch_stem(const StemParams &p, bool pre, hipStream_t s);
 const char *launch_dwpw(const DwPwParams &p, hipStream_t s);
 const char *launch_dwpw_mfma(const DwPwParams &p, hipStream_t s);  // the MFMA forms (dwpw_mfma.hip)
+const char *launch_ir(IrParams p, hipStream_t s);  // nullptr: the block does not fit the fused form
 const char *launch_chain(const ChainParams &p, hipStream_t s);
 
 }  // namespace zr
