@@ -190,6 +190,32 @@ int zr_track_seed_detections_async(const int32_t *d_count, const float *d_dets, 
                                    const uint32_t *d_frame_size, size_t n, const zr_track_cfg *cfg,
                                    float roi_grow, int roi_use_angle, zr_track_state *d_state,
                                    zr_track_state *d_seed_copy, zr_view_desc *d_views, void *hip_stream);
+/* HandTracker::track's bookkeeping (crates/zaru/src/hand/tracking.rs:115-219) for n video
+ * streams with their hands in HBM: stream s owns the hand slots [s * H, s * H + H) of d_state /
+ * d_ids / d_hroi (the hand's ROI, {cx, cy, w, h, rad}).  Called after zr_track_update_async has
+ * consumed the previous step's hand landmark estimate: drops lost hands (tracking.rs:116-127);
+ * when d_det_pending[s], filters stream s's palm detections (d_count / d_dets as
+ * zr_detect_post_async writes them, frame px) against the hands' ROIs (136-156) and starts a hand
+ * for each kept one, ROI = RotatedRect(det.rect.grow_rel(palm_grow), det.angle) (158-194, ids from
+ * d_next_id; past H slots a detection is dropped); removes hands whose ROI overlaps an earlier
+ * hand's with the reference's swap_remove sweep (196-208); and sets d_det_pending[s] when no hand
+ * is left or now_ms reached d_next_det[s] (advanced by interval_ms) -- this step's palm detection
+ * then counts at the next call (210-218).  Writes every slot's view (idle slots: an empty view),
+ * the hand counts and, per slot, the slot the hand had before the call (d_src, -1: new), so the
+ * caller can pair hands with the landmarks the update wrote.  Geometry as the host restatement
+ * (f32, no contraction): the same decisions as the host HandTracker given the same inputs. */
+typedef struct {
+    int slots;              /* H: hand slots per stream */
+    float iou_thresh;       /* tracking.rs:38 (0.3) */
+    float palm_grow;        /* tracking.rs:136 (1.5) */
+    double interval_ms;     /* redetection interval, tracking.rs:41 (300 ms) */
+    int aspect_w, aspect_h; /* the hand landmark network's aspect ratio */
+} zr_hand_cfg;
+int zr_hand_manage_async(zr_track_state *d_state, uint32_t *d_ids, float *d_hroi, int32_t *d_src,
+                         int32_t *d_nhands, uint32_t *d_next_id, double *d_next_det, int32_t *d_det_pending,
+                         const int32_t *d_count, const float *d_dets, size_t dcap,
+                         const uint32_t *d_frame_size, size_t n, const zr_hand_cfg *cfg, double now_ms,
+                         int init_clock, zr_view_desc *d_views, void *hip_stream);
 /* Cnn::estimate (nn/mod.rs:118-126) with a device-resident view table (frames: host array). */
 int zr_cnn_estimate_device_views_async(zr_session *s, const zr_frame *frames, size_t n_frames,
                                        const zr_view_desc *d_views, size_t n_views, float lo,

@@ -55,6 +55,8 @@ SIGNATURES = [
     ("zr_view_describe", _I, [_P, _SZ, _U32, _P]),
     ("zr_detect_post_async", _I, [_P, _P, _P, _P, _SZ, _P, _P, _P, _SZ, _P, _SZ, _U32, _U32, _P]),
     ("zr_track_seed_detections_async", _I, [_P, _P, _SZ, _P, _P, _P, _SZ, _P, _F, _I, _P, _P, _P, _P]),
+    ("zr_hand_manage_async", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P, _SZ, _P, C.c_double, _I,
+                                  _P, _P]),
     ("zr_debug_glibc_math", _I, [_I, _P, _P, _P, _SZ, _P]),
     ("zr_cnn_estimate_device_views_async", _I, [_P, _P, _SZ, _P, _SZ, _F, _F, _P, _P]),
     ("zr_jpeg_decoder_create", _I, [C.c_int, _P]),

@@ -7,6 +7,7 @@
 
 #include "detection.h"
 #include "hand_tracker.h"
+#include "device_hand_tracker.h"
 #include "landmark.h"
 #include "pipeline.h"
 #include "device_tracker.h"
@@ -287,6 +288,43 @@ PYBIND11_MODULE(_zaru_host, m) {
         .def_static("dedupe_rois", &HandTracker::dedupe_rois);
 
     // LandmarkTracker state on the device over n video streams
+    py::class_<DeviceHandTracker>(m, "DeviceHandTracker")
+        .def(py::init<size_t, int, int>(), py::arg("streams"), py::arg("slots") = 4, py::arg("device") = 0)
+        .def("set_redetect_interval", &DeviceHandTracker::set_redetect_interval, py::arg("ms"))
+        .def("set_iou_thresh", &DeviceHandTracker::set_iou_thresh)
+        .def("set_loss_threshold", &DeviceHandTracker::set_loss_threshold)
+        .def("inject_detections", &DeviceHandTracker::inject_detections)
+        .def("step", [](DeviceHandTracker &t, const std::vector<std::tuple<uint64_t, uint32_t, uint32_t, uint64_t>> &frames,
+                        double now_ms) {
+            std::vector<Image> im;
+            for (auto &f : frames) {
+                Image i;
+                i.rgba = reinterpret_cast<const uint8_t *>(std::get<0>(f));
+                i.width = std::get<1>(f);
+                i.height = std::get<2>(f);
+                i.row_stride = std::get<3>(f);
+                i.on_device = true;
+                im.push_back(i);
+            }
+            py::gil_scoped_release nogil;
+            t.step(im, now_ms);
+        }, py::arg("frames"), py::arg("now_ms"))
+        .def("synchronize", &DeviceHandTracker::synchronize, py::call_guard<py::gil_scoped_release>())
+        .def("hand_counts", &DeviceHandTracker::hand_counts)
+        .def("detection_pending", &DeviceHandTracker::detection_pending)
+        .def("hands", [](DeviceHandTracker &t, size_t s) {
+            py::list out;
+            for (auto &h : t.hands(s)) {
+                py::dict d;
+                d["id"] = h.id;
+                py::array_t<float> a({(py::ssize_t)(h.landmarks.size() / 3), (py::ssize_t)3});
+                std::memcpy(a.mutable_data(), h.landmarks.data(), h.landmarks.size() * 4);
+                d["landmarks"] = a;
+                d["view_rect"] = h.view_rect;
+                out.append(d);
+            }
+            return out;
+        });
     py::class_<DeviceTracker>(m, "DeviceTracker")
         .def(py::init([](const std::string &net, int device, float padding, float loss) {
                  return new DeviceTracker(landmark_net(net), device, padding, loss);

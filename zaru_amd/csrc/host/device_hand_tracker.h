@@ -1,0 +1,74 @@
+// device_hand_tracker.h -- HandTracker (crates/zaru/src/hand/tracking.rs:115-219) over n video
+// streams with every hand's state in HBM: each step runs, on one HIP stream,
+//   1. the LandmarkTracker update of every hand slot from the previous step's estimate
+//      (zr_track_update_async, kind "hand"),
+//   2. the bookkeeping -- drop lost hands, filter the previous step's palm detections against
+//      the hands' ROIs, start new hands, the swap_remove de-duplication, the redetection
+//      schedule (zr_hand_manage_async),
+//   3. the hand landmark network on every slot's view of this step's frame, and
+//   4. BlazePalm on every stream's frame with its device post-processing (zr_detect_post_async),
+//      whose detections step 2 consumes at the next step.
+// The host enqueues only: no host round trip per frame.  Stream s owns `slots` hand slots.
+// Schedule: a palm detection requested at step t is taken at step t + 1 -- the host HandTracker's
+// schedule when every detection finishes within one frame (HandTracker::wait_detection before
+// each track call), against which tests/test_gpu_device_hand_tracker.py checks it.
+#pragma once
+#include <memory>
+#include <vector>
+
+#include "detection.h"
+#include "landmark.h"
+
+namespace zh {
+
+class DeviceHandTracker {
+  public:
+    DeviceHandTracker(size_t streams, int slots = 4, int device = 0);
+    ~DeviceHandTracker();
+    DeviceHandTracker(const DeviceHandTracker &) = delete;
+    DeviceHandTracker &operator=(const DeviceHandTracker &) = delete;
+
+    void set_redetect_interval(double ms) { cfg_.interval_ms = ms; }
+    void set_iou_thresh(float t) { cfg_.iou_thresh = t; }
+    void set_loss_threshold(float t) { tcfg_.loss_thresh = t; }
+    // detections handed to stream s's next step as if its palm detection had produced them (test
+    // hook, the host HandTracker's inject_detections); replaces that step's palm result
+    void inject_detections(size_t s, const std::vector<Detection> &dets);
+    // one device-resident frame per stream; `now_ms` stands for Instant::now()
+    void step(const std::vector<Image> &frames, double now_ms);
+    void synchronize();
+    size_t streams() const { return n_; }
+    int slots() const { return cfg_.slots; }
+
+    struct HandData {  // tracking.rs:237-262
+        uint32_t id;
+        std::vector<float> landmarks;  // 21 x 3, frame px (the previous step's estimate)
+        RotatedRect view_rect;         // the hand's ROI
+    };
+    // after synchronize(): stream s's hands that have a result (HandTracker::hands)
+    std::vector<HandData> hands(size_t s);
+    std::vector<int32_t> hand_counts();  // every stream's hands, tracked or new
+    std::vector<int32_t> detection_pending();  // streams whose palm detection of the last step counts
+
+  private:
+    std::shared_ptr<const Cnn> palm_, hand_;
+    DetectorNetwork palm_net_ = DetectorNetwork::palm_lite();
+    LandmarkNetwork hand_net_ = LandmarkNetwork::hand_lite();
+    zr_hand_cfg cfg_{};
+    zr_track_cfg tcfg_{};
+    zr_detpost_cfg pcfg_{};
+    size_t n_ = 0, dcap_ = 8;
+    uint64_t steps_ = 0;
+    void *stream_ = nullptr;
+    uint32_t fw_ = 0, fh_ = 0;  // frame size the letterbox table was built for
+    DeviceArray<zr_track_state> state_;
+    DeviceArray<uint32_t> ids_, next_id_, fsize_;
+    DeviceArray<float> hroi_, lm_out_, outs_[4], palm_boxes_, palm_logits_, anchors_, lbox_, dets_;
+    DeviceArray<int32_t> src_, nhands_, det_pending_, count_;
+    DeviceArray<double> next_det_;
+    DeviceArray<zr_view_desc> views_;
+    std::vector<std::vector<Detection>> injected_;
+    std::vector<Rect> letterbox_;
+};
+
+}  // namespace zh

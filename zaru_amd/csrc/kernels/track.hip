@@ -226,7 +226,115 @@ __global__ __launch_bounds__(256) void seed_kernel(const SeedParams P) {
     if (P.seed_copy) P.seed_copy[i] = st;
 }
 
+// One thread per video stream: HandTracker::track's bookkeeping (tracking.rs:115-219) over the
+// stream's hand slots, in the reference's order.  Rect::iou and grow_rel as the host restates
+// them (geom_dev.h), so filter and de-duplication decide exactly as the host HandTracker does.
+__device__ void move_hand(const HandManageParams &P, int to, int from) {
+    P.state[to] = P.state[from];
+    P.ids[to] = P.ids[from];
+    P.src[to] = P.src[from];
+    for (int c = 0; c < 5; ++c) P.hroi[to * 5 + c] = P.hroi[from * 5 + c];
+}
+
+__global__ __launch_bounds__(64) void hand_manage_kernel(const HandManageParams P) {
+    const int s = blockIdx.x * 64 + threadIdx.x;
+    if (s >= P.S) return;
+    const int base = s * P.H;
+    if (P.init_clock) P.next_det[s] = P.now;
+    // 1. retain_mut: hands whose tracking was lost leave; the others' ROI is their updated_roi
+    int k = 0;
+    const int n = P.nhands[s];
+    for (int h = 0; h < n; ++h) {
+        const int i = base + h;
+        if (!P.state[i].active) continue;
+        const TrackState st = P.state[i];
+        const int j = base + k;
+        float r[5];
+        for (int c = 0; c < 5; ++c) r[c] = st.tracked ? st.updated[c] : P.hroi[i * 5 + c];
+        const uint32_t id = P.ids[i];
+        P.state[j] = st;
+        P.ids[j] = id;
+        P.src[j] = h;
+        for (int c = 0; c < 5; ++c) P.hroi[j * 5 + c] = r[c];
+        ++k;
+    }
+    // 2./3. the previous step's palm detections: keep those whose grown box overlaps no hand,
+    // then start a hand for each kept one (RotatedRect(grow_rel(1.5), angle), LandmarkTracker::set_roi)
+    if (P.det_pending[s]) {
+        const int cnt = min(P.count[s], P.dcap);
+        const int k0 = k;
+        uint32_t keep = 0;  // dcap <= 32
+        for (int d = 0; d < cnt; ++d) {
+            const float *dd = P.dets + ((int64_t)s * P.dcap + d) * 20;
+            const RRect g = grow_rel({dd[2], dd[3], dd[4], dd[5], 0.f}, P.grow);
+            bool ok = true;
+            for (int j = 0; j < k0 && ok; ++j) {
+                const float *r = P.hroi + (base + j) * 5;
+                ok = iou(r[0], r[1], r[2], r[3], g.cx, g.cy, g.w, g.h) < P.iou;
+            }
+            keep |= (ok ? 1u : 0u) << d;
+        }
+        for (int d = 0; d < cnt; ++d) {
+            if (!((keep >> d) & 1u) || k >= P.H) continue;  // past H slots: dropped (capacity)
+            const float *dd = P.dets + ((int64_t)s * P.dcap + d) * 20;
+            const RRect g = grow_rel({dd[2], dd[3], dd[4], dd[5], 0.f}, P.grow);
+            const int j = base + k;
+            TrackState st{};
+            st.roi[0] = g.cx;
+            st.roi[1] = g.cy;
+            st.roi[2] = g.w;
+            st.roi[3] = g.h;
+            st.roi[4] = dd[1];
+            st.active = 1;
+            st.frame_w = P.fsize[2 * s];
+            st.frame_h = P.fsize[2 * s + 1];
+            for (int c = 0; c < 5; ++c) P.hroi[j * 5 + c] = st.roi[c];
+            P.state[j] = st;
+            P.ids[j] = P.next_id[s]++;
+            P.src[j] = -1;
+            ++k;
+        }
+    }
+    // 4. for i in (0..len).rev(): the first earlier hand it overlaps removes it by swap_remove
+    for (int i = k - 1; i >= 0; --i) {
+        const float *a = P.hroi + (base + i) * 5;
+        for (int j = 0; j < i; ++j) {
+            const float *b = P.hroi + (base + j) * 5;
+            if (iou(a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]) >= P.iou) {
+                if (i != k - 1) move_hand(P, base + i, base + k - 1);
+                --k;
+                break;
+            }
+        }
+    }
+    // 5. start a detection when no hand is tracked or the redetect interval elapsed (none is
+    // running here: the previous one's result was consumed above)
+    const bool req = k == 0 || P.now >= P.next_det[s];
+    if (req) P.next_det[s] += P.interval;
+    P.det_pending[s] = req ? 1 : 0;
+    P.nhands[s] = k;
+    // this step's views; idle slots get a valid empty-frame view (the batched network stays in bounds)
+    for (int h = 0; h < P.H; ++h) {
+        const int i = base + h;
+        TrackState st = P.state[i];
+        if (h >= k) {
+            st = TrackState{};
+            st.roi[2] = st.roi[3] = 1.f;
+            st.frame_w = P.fsize[2 * s];
+            st.frame_h = P.fsize[2 * s + 1];
+            P.src[i] = -1;
+        }
+        next_view(st, P.views[i], s, P.asp_w, P.asp_h);
+        P.state[i] = st;
+    }
+}
+
 }  // namespace
+
+const char *launch_hand_manage(const HandManageParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(hand_manage_kernel, dim3((p.S + 63) / 64), dim3(64), 0, s, p);
+    return "hand_manage_kernel";
+}
 
 const char *launch_track(const TrackParams &p, hipStream_t s) {
     hipLaunchKernelGGL(track_kernel, dim3(p.n), dim3(256), 0, s, p);

@@ -730,6 +730,48 @@ int zr_track_seed_detections_async(const int32_t *d_count, const float *d_dets, 
     });
 }
 
+int zr_hand_manage_async(zr_track_state *d_state, uint32_t *d_ids, float *d_hroi, int32_t *d_src, int32_t *d_nhands,
+                         uint32_t *d_next_id, double *d_next_det, int32_t *d_det_pending, const int32_t *d_count,
+                         const float *d_dets, size_t dcap, const uint32_t *d_frame_size, size_t n,
+                         const zr_hand_cfg *cfg, double now_ms, int init_clock, zr_view_desc *d_views,
+                         void *hip_stream) {
+    return guarded([&]() -> int {
+        if (!d_state || !d_ids || !d_hroi || !d_src || !d_nhands || !d_next_id || !d_next_det || !d_det_pending ||
+            !d_count || !d_dets || !d_frame_size || !cfg || !d_views)
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument");
+        if (n == 0) return ZR_OK;
+        if (cfg->slots <= 0 || cfg->slots > 64 || dcap == 0 || dcap > 32 || (uint64_t)n * cfg->slots > (1u << 24) ||
+            cfg->aspect_w <= 0 || cfg->aspect_h <= 0 || !(cfg->interval_ms >= 0.0) || !(cfg->palm_grow >= 0.f))
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "bad hand tracker configuration");
+        zr::HandManageParams p{};
+        p.state = reinterpret_cast<zr::TrackState *>(d_state);
+        p.ids = d_ids;
+        p.hroi = d_hroi;
+        p.src = d_src;
+        p.nhands = d_nhands;
+        p.next_id = d_next_id;
+        p.next_det = d_next_det;
+        p.det_pending = d_det_pending;
+        p.count = d_count;
+        p.dets = d_dets;
+        p.fsize = d_frame_size;
+        p.views = reinterpret_cast<zr::ViewDesc *>(d_views);
+        p.S = (int)n;
+        p.H = cfg->slots;
+        p.dcap = (int)dcap;
+        p.iou = cfg->iou_thresh;
+        p.grow = cfg->palm_grow;
+        p.now = now_ms;
+        p.interval = cfg->interval_ms;
+        p.init_clock = init_clock ? 1 : 0;
+        p.asp_w = cfg->aspect_w;
+        p.asp_h = cfg->aspect_h;
+        zr::launch_hand_manage(p, (hipStream_t)hip_stream);
+        HIP_TRY(hipGetLastError());
+        return ZR_OK;
+    });
+}
+
 int zr_view_describe(const zr_view *views, size_t n, uint32_t frame, zr_view_desc *out) {
     return guarded([&]() -> int {
         if (!views || !out) return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument");

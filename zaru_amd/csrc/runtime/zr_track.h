@@ -79,6 +79,33 @@ struct SeedParams {
     ViewDesc *views;         // [N * R] out
 };
 const char *launch_seed(const SeedParams &p, hipStream_t s);
+// HandTracker::track's bookkeeping (crates/zaru/src/hand/tracking.rs:115-219) per video stream,
+// on the device (track.hip): stream s owns hand slots [s * H, s * H + H) in hand order.  After
+// the landmark update of the previous step: drop lost hands (retain, 116-127), filter the palm
+// detections the previous step produced against the hands' ROIs (136-156), start a hand for
+// every kept one (158-194), remove hands whose ROI overlaps an earlier hand's (swap_remove sweep,
+// 196-208), and decide whether this step's palm detection counts (210-218).
+struct HandManageParams {
+    TrackState *state;       // [S * H] hand slots (the track update's output)
+    uint32_t *ids;           // [S * H]
+    float *hroi;             // [S * H][5] the hand's ROI (tracking.rs: TrackedHand::roi)
+    int32_t *src;            // [S * H] out: slot of the hand before this call (-1: new hand)
+    int32_t *nhands;         // [S]
+    uint32_t *next_id;       // [S]
+    double *next_det;        // [S] redetection clock (ms)
+    int32_t *det_pending;    // [S] in: count/dets hold this stream's detections; out: this step's counts
+    const int32_t *count;    // [S] detections (det_post)
+    const float *dets;       // [S][dcap][20]
+    const uint32_t *fsize;   // [S][2]
+    ViewDesc *views;         // [S * H] out: the views this step's landmark estimate samples
+    int S, H, dcap;
+    float iou, grow;
+    double now, interval;
+    int init_clock;          // 1: next_det = now first (the reference starts the clock at construction)
+    int asp_w, asp_h;
+};
+const char *launch_hand_manage(const HandManageParams &p, hipStream_t s);
+
 // fn: 0 sinf, 1 cosf, 2 expf, 3 atanf, 4 atan2f(a, b) -- glibc_math.h on the device
 const char *launch_glibc_math(int fn, const float *a, const float *b, float *out, int64_t n, hipStream_t s);
 
