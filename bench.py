@@ -554,6 +554,7 @@ def main():
         out["face_next"] = next_line(H, args, device, side_traffic.get("face_next"))
     if world == 1 and args.workload == "face" and not args.no_tracking:
         out["tracking"] = tracking_line(H, args, device, wl)
+        out["hand_tracking"] = hand_tracking_line(H, args, device, wl)
     if world == 1 and args.workload == "face" and not args.no_c5:
         out["config5"] = c5_line(H, args, device, wl)
     if world == 1 and args.workload == "face" and not args.no_jpeg:
@@ -633,6 +634,39 @@ def tracking_line(H, args, device, wl):
             "pipeline_roofline": {"model": "SURVEY.md §8d FaceMesh bytes + 192^2 preprocessing per face",
                                   "bytes_per_face": round(bpf), "achieved_GBs": round(fps * bpf / 1e9, 1),
                                   "frac": round(fps * bpf / 1e9 / HBM_PEAK_GBS, 4)}}
+
+
+def hand_tracking_line(H, args, device, wl, streams=256, slots=4):
+    """SURVEY §8f-3 (HandTracker): DeviceHandTracker over `streams` video streams (the face
+    workload's 1080p frames), 4 hand slots each, seeded with 4 injected palm detections per
+    stream; each step = the hand landmark update + the bookkeeping kernel (filter, new hands,
+    swap_remove de-duplication, redetection schedule) + hand landmarks on every slot + BlazePalm
+    with device post-processing on every frame, no host round trip.  Loss threshold -1 keeps
+    the synthetic hands tracked.  value = tracked hands per second."""
+    import torch
+    fs = wl.fs
+    frames = wl.flist[:streams]
+    tr = H.DeviceHandTracker(len(frames), slots, device)
+    tr.set_loss_threshold(-1.0)
+    for s, (y, x) in enumerate(fs.pos[:len(frames)]):
+        tr.inject_detections(s, [H.Detection(0.9, H.Rect.from_center(x + 96.0 + 384.0 * (k % 2), y + 96.0 + 384.0 * (k // 2),
+                                                                     60.0, 60.0), 0.0) for k in range(slots)])
+    ms = 1000.0 / 30.0
+    for k in range(3):
+        tr.step(frames, k * ms)
+    tr.synchronize()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.tracking_steps):
+        tr.step(frames, (3 + k) * ms)
+    tr.synchronize()
+    elapsed = time.perf_counter() - t0
+    hands = int(sum(tr.hand_counts()))
+    return {"metric": "tracked hands/sec, HandTracker video loop with device-resident state (hand landmarks "
+                      "per hand + BlazePalm per frame + bookkeeping on the device)",
+            "value": round(hands * args.tracking_steps / elapsed, 1), "unit": "hands/s", "streams": len(frames),
+            "slots": slots, "hands": hands, "steps": args.tracking_steps,
+            "ms_per_step": round(1e3 * elapsed / args.tracking_steps, 3)}
 
 
 def jpeg_line(args, device, n_distinct=32, n_decodes=512, threads=16):
