@@ -242,6 +242,10 @@ typedef struct {
     uint32_t bw[3], bh[3], qsel[3];
     uint16_t quant[4][64]; /* natural order */
 } zr_jpeg_layout;
+/* Decodes so far whose Huffman stage ran on the device (streams with restart intervals: one
+ * thread per interval) and on the host; *corrupt (may be NULL; waits for the last decode) is 1
+ * when a device-decoded stream held an invalid Huffman code or AC index since creation. */
+int zr_jpeg_decoder_status(zr_jpeg_decoder *d, uint64_t *gpu_entropy, uint64_t *host_entropy, int *corrupt);
 int zr_jpeg_coefficients(const uint8_t *jpeg, size_t len, int16_t *coef, size_t cap_blocks,
                          zr_jpeg_layout *layout);
 

@@ -9,6 +9,8 @@ image, so parity with it is unpinned (it differs from libjpeg-turbo by +-1 in pl
 
 Inputs are synthetic (seeded noise, gradients, a face crop of the reference's own test image),
 encoded by Pillow at several sizes, qualities, chroma subsamplings and restart intervals.
+Streams with restart intervals take the device Huffman path (kernels/jpeg_huff.hip); the bar
+is the same byte equality.
 """
 import io
 import os
@@ -61,6 +63,10 @@ CASES = [
     (45, 131, 85, 1, {}),
     (120, 160, 75, 2, {"restart_marker_blocks": 3}),
     (97, 203, 100, 0, {"restart_marker_rows": 1}),
+    # restart intervals: the Huffman stage runs on the device, one thread per interval
+    (1080, 1920, 90, 2, {"restart_marker_rows": 1}),
+    (1080, 1920, 75, 0, {"restart_marker_blocks": 7}),
+    (720, 1280, 95, 1, {"restart_marker_rows": 2}),
 ]
 
 
@@ -155,3 +161,35 @@ def test_truncated_scan_is_decoded_or_rejected(dec):
     except ZaruError:
         return
     assert out.shape == (64, 64, 4)
+
+
+def test_restart_streams_decode_on_the_device(dec):
+    """Streams with >= 8 restart intervals are entropy-decoded on the GPU (decoder status), with
+    no corrupt interval flagged; streams without DRI stay on the host path."""
+    from zaru_amd.jpeg import JpegDecoder
+    d = JpegDecoder(0)
+    try:
+        with_rst = encode(synthetic(1080, 1920, 5), quality=90, restart_marker_rows=1)
+        plain = encode(synthetic(1080, 1920, 5), quality=90)
+        g = synthetic(200, 300, 9)[..., 0]
+        gray_rst = encode(g, quality=85, restart_marker_blocks=5)
+        for data in (with_rst, plain, gray_rst):
+            assert np.array_equal(d.decode(data), libjpeg_turbo_rgba(data))
+        gpu, host, corrupt = d.status()
+        assert (gpu, host, corrupt) == (2, 1, 0)
+    finally:
+        d.close()
+
+
+def test_restart_stream_cut_mid_scan(dec):
+    """A restart-interval stream cut inside the scan no longer has one RSTn per interval: it
+    takes the host path, which pads with zero bits or rejects it, and never reads past the
+    buffer."""
+    from zaru_amd._lib import ZaruError
+    data = encode(synthetic(240, 320, 4), quality=90, restart_marker_rows=1)
+    cut = data[: len(data) * 2 // 3]
+    try:
+        out = dec.decode(cut)
+    except ZaruError:
+        return
+    assert out.shape == (240, 320, 4)

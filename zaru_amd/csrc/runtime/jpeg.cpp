@@ -3,11 +3,14 @@
 // device half (kernels/jpeg.hip) turns into RGBA8 frames in HBM.  Entropy decoding is bit-serial
 // within a scan, so it stays on a CPU core, as in every GPU JPEG pipeline; the pixel work
 // (IDCT, upsampling, colour conversion: ~all of libjpeg-turbo's decode time) runs on the GPU.
+// Streams with restart intervals (DRI) are entropy-decoded on the GPU too, one thread per
+// interval (kernels/jpeg_huff.hip): only the scan bytes cross PCIe then.
 // Supported: baseline sequential DCT (SOF0/SOF1), 8-bit samples, 1 or 3 components with luma
 // sampling 1x1 / 2x1 / 2x2 over 1x1 chroma, one interleaved scan, restart intervals.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -265,7 +268,13 @@ struct zr_jpeg_decoder {
     size_t coef_cap = 0;  // blocks
     uint8_t *d_planes = nullptr;
     size_t planes_cap = 0;
-    hipEvent_t staged = nullptr;  // the last H2D copy out of h_coef has completed
+    // device entropy decoding (streams with restart intervals): tables + interval offsets + scan
+    // bytes staged in pinned memory and copied once per frame
+    uint8_t *h_stage = nullptr, *d_stage = nullptr;
+    size_t stage_cap = 0;
+    int *d_err = nullptr;         // set by jpeg_huff_kernel on a corrupt interval
+    uint64_t n_gpu = 0, n_host = 0;
+    hipEvent_t staged = nullptr;  // the last H2D copy out of h_coef / h_stage has completed
     hipEvent_t done = nullptr;    // the last decode's kernels (readers of d_coef / d_planes) completed
 };
 
@@ -361,6 +370,52 @@ void entropy_decode(const Header &hd, const zr::JpegParams &P, const uint8_t *jp
     }
 }
 
+void dev_table(const Huff &h, zr::JpegHuffTable &t) {
+    std::memset(&t, 0, sizeof t);
+    if (!h.present) return;
+    std::memcpy(t.look, h.look, sizeof t.look);
+    std::memcpy(t.fast_ac, h.fast_ac, sizeof t.fast_ac);
+    std::memcpy(t.maxcode, h.maxcode, sizeof t.maxcode);
+    std::memcpy(t.valoff, h.valoff, sizeof t.valoff);
+    std::memcpy(t.vals, h.vals, sizeof t.vals);
+}
+
+// Byte offsets (from scan_begin) where each restart interval's entropy-coded data starts, plus the
+// end of the scan (the EOI / first non-RST marker); false when the stream does not have exactly
+// one interval per `restart` MCUs -- the caller then decodes on the host, which reports errors.
+bool restart_intervals(const uint8_t *d, size_t n, size_t begin, int n_iv, std::vector<int32_t> &off) {
+    off.clear();
+    off.push_back(0);
+    size_t p = begin;
+    while (p + 1 < n) {
+        const uint8_t *f = static_cast<const uint8_t *>(std::memchr(d + p, 0xFF, n - 1 - p));
+        if (!f) break;
+        p = (size_t)(f - d);
+        const uint8_t nx = d[p + 1];
+        if (nx == 0x00 || nx == 0xFF) {  // stuffed byte / fill byte
+            p += nx == 0x00 ? 2 : 1;
+            continue;
+        }
+        if (nx >= 0xD0 && nx <= 0xD7) {
+            off.push_back((int32_t)(p + 2 - begin));
+            p += 2;
+            continue;
+        }
+        break;  // EOI or another marker ends the scan
+    }
+    const size_t end = p + 1 < n ? p : n;
+    off.push_back((int32_t)(end - begin));
+    return (int)off.size() == n_iv + 1 && end - begin < ((size_t)1 << 31);
+}
+
+bool gpu_entropy_enabled() {  // ZARU_JPEG_HOST_ENTROPY=1 keeps every decode on the host (A/B)
+    static const bool on = [] {
+        const char *e = std::getenv("ZARU_JPEG_HOST_ENTROPY");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
+
 }  // namespace
 
 extern "C" {
@@ -381,6 +436,12 @@ int zr_jpeg_decoder_create(int device, zr_jpeg_decoder **out) {
             delete d;
             return err(ZR_ERR_DEVICE, "hipEventCreate failed");
         }
+        if (hipMalloc((void **)&d->d_err, sizeof(int)) != hipSuccess || hipMemset(d->d_err, 0, sizeof(int)) != hipSuccess) {
+            (void)hipEventDestroy(d->staged);
+            (void)hipEventDestroy(d->done);
+            delete d;
+            return err(ZR_ERR_DEVICE, "hipMalloc failed");
+        }
         *out = d;
         return ZR_OK;
     } catch (...) {
@@ -397,7 +458,29 @@ void zr_jpeg_decoder_destroy(zr_jpeg_decoder *d) {
     (void)hipHostFree(d->h_coef);
     (void)hipFree(d->d_coef);
     (void)hipFree(d->d_planes);
+    (void)hipHostFree(d->h_stage);
+    (void)hipFree(d->d_stage);
+    (void)hipFree(d->d_err);
     delete d;
+}
+
+int zr_jpeg_decoder_status(zr_jpeg_decoder *d, uint64_t *gpu_entropy, uint64_t *host_entropy, int *corrupt) {
+    try {
+        if (!d) return err(ZR_ERR_INVALID_ARGUMENT, "null decoder");
+        std::lock_guard<std::mutex> g(d->mu);
+        if (gpu_entropy) *gpu_entropy = d->n_gpu;
+        if (host_entropy) *host_entropy = d->n_host;
+        if (corrupt) {
+            int e = 0;
+            if (hipSetDevice(d->device) != hipSuccess || hipEventSynchronize(d->done) != hipSuccess ||
+                hipMemcpy(&e, d->d_err, sizeof e, hipMemcpyDeviceToHost) != hipSuccess)
+                return err(ZR_ERR_DEVICE, "jpeg: status read failed");
+            *corrupt = e;
+        }
+        return ZR_OK;
+    } catch (...) {
+        return err(ZR_ERR_INTERNAL, "jpeg: internal error");
+    }
 }
 
 int zr_jpeg_info(const uint8_t *jpeg, size_t len, uint32_t *width, uint32_t *height) {
@@ -486,14 +569,69 @@ int zr_jpeg_decode_async(zr_jpeg_decoder *dec, const uint8_t *jpeg, size_t len, 
             if (hipMalloc((void **)&dec->d_planes, cap) != hipSuccess) return err(ZR_ERR_DEVICE, "jpeg: out of memory");
             dec->planes_cap = cap;
         }
-        entropy_decode(hd, P, jpeg, len, dec->h_coef);
         hipStream_t st = (hipStream_t)hip_stream;
-        // d_coef / d_planes are reused: on another stream the previous decode's IDCT and colour
-        // kernels may still read them, so this stream waits for them before overwriting
-        if (hipStreamWaitEvent(st, dec->done, 0) != hipSuccess ||
-            hipMemcpyAsync(dec->d_coef, dec->h_coef, (size_t)blocks * 128, hipMemcpyHostToDevice, st) != hipSuccess ||
-            hipEventRecord(dec->staged, st) != hipSuccess)
-            return err(ZR_ERR_DEVICE, "jpeg: coefficient upload failed");
+        const int mcux = P.bw[0] / hd.comp[0].h, nmcu = mcux * (P.bh[0] / hd.comp[0].v);
+        const int n_iv = hd.restart > 0 ? (nmcu + hd.restart - 1) / hd.restart : 0;
+        std::vector<int32_t> ivo;
+        if (gpu_entropy_enabled() && n_iv >= 8 && restart_intervals(jpeg, len, hd.scan_begin, n_iv, ivo)) {
+            // device entropy decoding: [8 tables][interval offsets][scan bytes] in one copy
+            const size_t tb = 8 * sizeof(zr::JpegHuffTable), ob = ((size_t)(n_iv + 1) * 4 + 15) / 16 * 16;
+            const size_t db = (size_t)ivo.back(), need = tb + ob + db + 48;  // + the reader's look-ahead words
+            if (need > dec->stage_cap) {
+                if (hipEventSynchronize(dec->done) != hipSuccess) return err(ZR_ERR_DEVICE, "event sync failed");
+                (void)hipHostFree(dec->h_stage);
+                (void)hipFree(dec->d_stage);
+                dec->h_stage = nullptr;
+                dec->d_stage = nullptr;
+                dec->stage_cap = 0;
+                const size_t cap = need + need / 4;
+                if (hipHostMalloc((void **)&dec->h_stage, cap) != hipSuccess ||
+                    hipMalloc((void **)&dec->d_stage, cap) != hipSuccess)
+                    return err(ZR_ERR_DEVICE, "jpeg: out of memory");
+                dec->stage_cap = cap;
+            }
+            auto *tabs = reinterpret_cast<zr::JpegHuffTable *>(dec->h_stage);
+            for (int t = 0; t < 4; t++) {
+                dev_table(hd.dc[t], tabs[t]);
+                dev_table(hd.ac[t], tabs[4 + t]);
+            }
+            std::memcpy(dec->h_stage + tb, ivo.data(), (size_t)(n_iv + 1) * 4);
+            std::memcpy(dec->h_stage + tb + ob, jpeg + hd.scan_begin, db);
+            if (hipStreamWaitEvent(st, dec->done, 0) != hipSuccess ||
+                hipMemcpyAsync(dec->d_stage, dec->h_stage, need, hipMemcpyHostToDevice, st) != hipSuccess ||
+                hipEventRecord(dec->staged, st) != hipSuccess)
+                return err(ZR_ERR_DEVICE, "jpeg: scan upload failed");
+            zr::JpegHuffParams hp{};
+            hp.tables = reinterpret_cast<const zr::JpegHuffTable *>(dec->d_stage);
+            hp.iv_off = reinterpret_cast<const int32_t *>(dec->d_stage + tb);
+            hp.data = dec->d_stage + tb + ob;
+            hp.coef = dec->d_coef;
+            hp.n_iv = n_iv;
+            hp.restart = hd.restart;
+            hp.nmcu = nmcu;
+            hp.mcux = mcux;
+            hp.ncomp = hd.ncomp;
+            for (int c = 0; c < hd.ncomp; c++) {
+                hp.ch[c] = hd.comp[c].h;
+                hp.cv[c] = hd.comp[c].v;
+                hp.td[c] = hd.comp[c].td;
+                hp.ta[c] = hd.comp[c].ta;
+                hp.coef_off[c] = P.coef_off[c];
+                hp.bw[c] = P.bw[c];
+            }
+            hp.error = dec->d_err;
+            zr::launch_jpeg_huff(hp, st);
+            dec->n_gpu++;
+        } else {
+            entropy_decode(hd, P, jpeg, len, dec->h_coef);
+            // d_coef / d_planes are reused: on another stream the previous decode's IDCT and
+            // colour kernels may still read them, so this stream waits for them first
+            if (hipStreamWaitEvent(st, dec->done, 0) != hipSuccess ||
+                hipMemcpyAsync(dec->d_coef, dec->h_coef, (size_t)blocks * 128, hipMemcpyHostToDevice, st) != hipSuccess ||
+                hipEventRecord(dec->staged, st) != hipSuccess)
+                return err(ZR_ERR_DEVICE, "jpeg: coefficient upload failed");
+            dec->n_host++;
+        }
         P.coef = dec->d_coef;
         P.planes = dec->d_planes;
         P.out = d_rgba;

@@ -1,7 +1,8 @@
 """JPEG frame source over the C ABI: baseline JPEG bytes -> RGBA8 frames in
 HBM, byte-identical to the reference's libjpeg-turbo backend (crates/zaru-image/src/jpeg.rs:
-164-182; `decode_jpeg` returns RGBA with alpha 255).  Entropy decoding runs on the calling
-thread, the pixel stages on the GPU (kernels/jpeg.hip)."""
+164-182; `decode_jpeg` returns RGBA with alpha 255).  Streams with restart intervals are
+entropy-decoded on the GPU, one thread per interval (kernels/jpeg_huff.hip); others on the
+calling thread.  The pixel stages always run on the GPU (kernels/jpeg.hip)."""
 from __future__ import annotations
 
 import ctypes as C
@@ -60,6 +61,12 @@ class JpegDecoder:
         """Enqueue the decode of `data` into the device buffer at `d_rgba` (RGBA8 rows of
         `row_stride` bytes) on `stream` (default stream when None)."""
         check(lib().zr_jpeg_decode_async(self._h, data, len(data), d_rgba, row_stride, stream))
+
+    def status(self):
+        """(device entropy decodes, host entropy decodes, corrupt flag) since creation."""
+        g, h, c = C.c_uint64(), C.c_uint64(), C.c_int()
+        check(lib().zr_jpeg_decoder_status(self._h, C.byref(g), C.byref(h), C.byref(c)))
+        return g.value, h.value, c.value
 
     def decode(self, data: bytes):
         """Decode to a host numpy array [H, W, 4] (test / convenience path)."""
