@@ -224,17 +224,25 @@ int zr_cnn_estimate_device_views_async(zr_session *s, const zr_frame *frames, si
 /* ---- JPEG frame source --------------------------------------------------
  * Replaces decode_jpeg (crates/zaru-image/src/jpeg.rs:107-182) for its libjpeg-turbo backend
  * (turbojpeg 0.5.3: accurate integer IDCT, fancy upsampling, TJPF_RGBA output): the frame is
- * decoded straight into an RGBA8 device buffer, byte-identical to libjpeg-turbo.  Entropy
- * decoding runs on the calling thread; dequantisation, IDCT, upsampling and colour conversion
- * are enqueued on `hip_stream`.  Baseline 8-bit JPEG, 1 or 3 components, 4:4:4 / 4:2:2 / 4:2:0,
- * one interleaved scan, restart markers.  A decoder may be reused; calls on one decoder are
- * serialised (its coefficient staging is reused once the previous upload completed). */
+ * decoded straight into an RGBA8 device buffer, byte-identical to libjpeg-turbo.  Streams with
+ * restart intervals (DRI, >= 8 intervals, each 64-interval range within a workgroup's LDS) are
+ * Huffman-decoded on the device, one lane per interval; the others on the calling thread.
+ * Dequantisation, IDCT, upsampling and colour conversion are enqueued on `hip_stream`.  Baseline
+ * 8-bit JPEG, 1 or 3 components, 4:4:4 / 4:2:2 / 4:2:0, one interleaved scan, restart markers.
+ * A decoder may be reused; calls on one decoder are serialised (its staging is reused once the
+ * previous upload completed). */
 typedef struct zr_jpeg_decoder zr_jpeg_decoder;
 int zr_jpeg_decoder_create(int device, zr_jpeg_decoder **out);
 void zr_jpeg_decoder_destroy(zr_jpeg_decoder *d);
 int zr_jpeg_info(const uint8_t *jpeg, size_t len, uint32_t *width, uint32_t *height);
 int zr_jpeg_decode_async(zr_jpeg_decoder *d, const uint8_t *jpeg, size_t len, uint8_t *d_rgba,
                          size_t row_stride, void *hip_stream);
+/* n frames (<= 4096) in one call: frame i from jpegs[i] (lens[i] bytes) into d_rgba[i].  Every
+ * frame is parsed before anything is enqueued (an error names the frame); the device-decodable
+ * frames share one Huffman launch, so a multi-camera ingest fills the GPU with one call instead
+ * of one small launch per frame.  zr_jpeg_decode_async is the n = 1 case. */
+int zr_jpeg_decode_batch_async(zr_jpeg_decoder *d, size_t n, const uint8_t *const *jpegs, const size_t *lens,
+                               uint8_t *const *d_rgba, const size_t *row_strides, void *hip_stream);
 /* Host-only half (no GPU): the frame's block layout and, when `coef` is given, its quantised
  * coefficients ([component][by][bx][64], natural order; cap_blocks >= layout->total_blocks). */
 typedef struct {
@@ -242,8 +250,8 @@ typedef struct {
     uint32_t bw[3], bh[3], qsel[3];
     uint16_t quant[4][64]; /* natural order */
 } zr_jpeg_layout;
-/* Decodes so far whose Huffman stage ran on the device (streams with restart intervals: one
- * thread per interval) and on the host; *corrupt (may be NULL; waits for the last decode) is 1
+/* Frames decoded so far whose Huffman stage ran on the device (streams with restart intervals:
+ * one lane per interval) and on the host; *corrupt (may be NULL; waits for the last decode) is 1
  * when a device-decoded stream held an invalid Huffman code or AC index since creation. */
 int zr_jpeg_decoder_status(zr_jpeg_decoder *d, uint64_t *gpu_entropy, uint64_t *host_entropy, int *corrupt);
 int zr_jpeg_coefficients(const uint8_t *jpeg, size_t len, int16_t *coef, size_t cap_blocks,

@@ -63,9 +63,13 @@ CASES = [
     (45, 131, 85, 1, {}),
     (120, 160, 75, 2, {"restart_marker_blocks": 3}),
     (97, 203, 100, 0, {"restart_marker_rows": 1}),
-    # restart intervals: the Huffman stage runs on the device, one thread per interval
-    (1080, 1920, 90, 2, {"restart_marker_rows": 1}),
+    # restart intervals: the Huffman stage runs on the device, one lane per interval
+    (1080, 1920, 90, 2, {"restart_marker_blocks": 1}),
+    (1080, 1920, 90, 2, {"restart_marker_blocks": 4}),
     (1080, 1920, 75, 0, {"restart_marker_blocks": 7}),
+    (720, 1280, 95, 1, {"restart_marker_blocks": 2}),
+    # long intervals (a 64-interval range over the LDS budget): host entropy decoding
+    (1080, 1920, 90, 2, {"restart_marker_rows": 1}),
     (720, 1280, 95, 1, {"restart_marker_rows": 2}),
 ]
 
@@ -164,19 +168,71 @@ def test_truncated_scan_is_decoded_or_rejected(dec):
 
 
 def test_restart_streams_decode_on_the_device(dec):
-    """Streams with >= 8 restart intervals are entropy-decoded on the GPU (decoder status), with
-    no corrupt interval flagged; streams without DRI stay on the host path."""
+    """Streams with >= 8 restart intervals short enough for a workgroup's LDS are entropy-decoded
+    on the GPU (decoder status), with no corrupt interval flagged; streams without DRI, and ones
+    whose intervals are too long, stay on the host path."""
     from zaru_amd.jpeg import JpegDecoder
     d = JpegDecoder(0)
     try:
-        with_rst = encode(synthetic(1080, 1920, 5), quality=90, restart_marker_rows=1)
+        with_rst = encode(synthetic(1080, 1920, 5), quality=90, restart_marker_blocks=4)
+        long_rst = encode(synthetic(1080, 1920, 5), quality=90, restart_marker_rows=1)
         plain = encode(synthetic(1080, 1920, 5), quality=90)
         g = synthetic(200, 300, 9)[..., 0]
         gray_rst = encode(g, quality=85, restart_marker_blocks=5)
-        for data in (with_rst, plain, gray_rst):
+        for data in (with_rst, long_rst, plain, gray_rst):
             assert np.array_equal(d.decode(data), libjpeg_turbo_rgba(data))
         gpu, host, corrupt = d.status()
-        assert (gpu, host, corrupt) == (2, 1, 0)
+        assert (gpu, host, corrupt) == (2, 2, 0)
+    finally:
+        d.close()
+
+
+def _scan_start(data):
+    i = data.index(b"\xff\xda")
+    return i + 2 + int.from_bytes(data[i + 2:i + 4], "big")
+
+
+def test_restart_stream_with_fill_bytes(dec):
+    """0xFF fill bytes in front of every RSTn (T.81 B.1.1.2 allows any number): the interval ends
+    at the first of them, as in the host reader, and the output still equals libjpeg-turbo's."""
+    from zaru_amd.jpeg import JpegDecoder
+    data = encode(synthetic(480, 640, 8), quality=90, restart_marker_blocks=2)
+    k = _scan_start(data)
+    scan = data[k:]
+    for n in range(8):
+        m = bytes([0xFF, 0xD0 + n])
+        scan = scan.replace(m, b"\xff\xff" + m)
+    filled = data[:k] + scan
+    assert len(filled) > len(data)
+    d = JpegDecoder(0)
+    try:
+        assert np.array_equal(d.decode(filled), libjpeg_turbo_rgba(data))
+        assert d.status() == (1, 0, 0)
+    finally:
+        d.close()
+
+
+def test_restart_stream_corrupt_interval_is_flagged(dec):
+    """A corrupt interval (an invalid Huffman code) is flagged by the device decoder (status
+    `corrupt`), the frame still decodes without a fault, and the next good frame is clean."""
+    from zaru_amd.jpeg import JpegDecoder
+    data = encode(synthetic(480, 640, 8), quality=90, restart_marker_blocks=2)
+    k = _scan_start(data)
+    bad = bytearray(data)
+    # inside the third interval, away from its markers: stuffed 0xFF pairs, i.e. a run of 64 one
+    # bits -- longer than any code (T.81 C: the all-ones code is never assigned)
+    r = [i for i in range(k, len(data) - 1) if data[i] == 0xFF and 0xD0 <= data[i + 1] <= 0xD7]
+    p = (r[1] + r[2]) // 2
+    while data[p - 1] == 0xFF:
+        p += 1
+    assert p + 16 < r[2]
+    bad[p:p + 16] = b"\xff\x00" * 8
+    d = JpegDecoder(0)
+    try:
+        out = d.decode(bytes(bad))
+        assert out.shape == (480, 640, 4)
+        assert d.status()[2] == 1
+        assert np.array_equal(d.decode(data), libjpeg_turbo_rgba(data))
     finally:
         d.close()
 
@@ -193,3 +249,50 @@ def test_restart_stream_cut_mid_scan(dec):
     except ZaruError:
         return
     assert out.shape == (240, 320, 4)
+
+
+def test_batch_decode_mixed_frames(dec):
+    """zr_jpeg_decode_batch_async: frames of different sizes, subsamplings and entropy paths
+    (restart intervals -> one shared device Huffman launch; no DRI / long intervals -> host) in
+    one call, each equal to libjpeg-turbo's decode."""
+    from zaru_amd._lib import DeviceBuffer, lib
+    from zaru_amd.jpeg import JpegDecoder
+    specs = [((1080, 1920), 90, 2, {"restart_marker_blocks": 4}),
+             ((480, 640), 85, 0, {}),
+             ((720, 1280), 95, 1, {"restart_marker_blocks": 2}),
+             ((33, 17), 90, 2, {}),
+             ((1080, 1920), 90, 2, {"restart_marker_rows": 1}),
+             ((240, 320), 75, 2, {"restart_marker_blocks": 1})]
+    datas = [encode(synthetic(h, w, 300 + i), quality=q, subsampling=sub, **kw)
+             for i, ((h, w), q, sub, kw) in enumerate(specs)]
+    datas.append(encode(synthetic(200, 300, 9)[..., 0], quality=85, restart_marker_blocks=5))
+    shapes = [(h, w) for (h, w), *_ in specs] + [(200, 300)]
+    bufs = [DeviceBuffer(h * w * 4) for h, w in shapes]
+    d = JpegDecoder(0)
+    try:
+        d.decode_batch_into(datas, [b.ptr for b in bufs], [w * 4 for _, w in shapes])
+        lib().zr_stream_synchronize(None)
+        for i, (data, (h, w)) in enumerate(zip(datas, shapes)):
+            assert np.array_equal(bufs[i].download((h, w, 4), "uint8"), libjpeg_turbo_rgba(data)), i
+        assert d.status() == (4, 3, 0)
+    finally:
+        d.close()
+
+
+def test_batch_decode_rejects_a_bad_frame_before_enqueueing(dec):
+    from zaru_amd._lib import DeviceBuffer, ZaruError
+    from zaru_amd.jpeg import JpegDecoder
+    good = encode(synthetic(64, 64, 1), quality=90, restart_marker_blocks=1)
+    buf = DeviceBuffer(64 * 64 * 4 * 3)
+    d = JpegDecoder(0)
+    try:
+        with pytest.raises(ZaruError, match="frame 1"):
+            d.decode_batch_into([good, b"not a jpeg", good], [buf.ptr + i * 64 * 64 * 4 for i in range(3)], [256] * 3)
+        assert d.status()[:2] == (0, 0)
+        d.decode_batch_into([good] * 3, [buf.ptr + i * 64 * 64 * 4 for i in range(3)], [256] * 3)
+        want = libjpeg_turbo_rgba(good)
+        got = buf.download((3, 64, 64, 4), "uint8")
+        for i in range(3):
+            assert np.array_equal(got[i], want)
+    finally:
+        d.close()

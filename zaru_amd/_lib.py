@@ -63,6 +63,7 @@ SIGNATURES = [
     ("zr_jpeg_decoder_destroy", None, [_P]),
     ("zr_jpeg_info", _I, [_P, _SZ, _P, _P]),
     ("zr_jpeg_decode_async", _I, [_P, _P, _SZ, _P, _SZ, _P]),
+    ("zr_jpeg_decode_batch_async", _I, [_P, _SZ, _P, _P, _P, _P, _P]),
     ("zr_jpeg_coefficients", _I, [_P, _SZ, _P, _SZ, _P]),
     ("zr_jpeg_decoder_status", _I, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(_I)]),
     ("zr_session_stats", _I, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(_SZ)]),

@@ -1,5 +1,5 @@
 // jpeg_huff.hip -- baseline JPEG Huffman entropy decoding on the device for
-// streams with restart intervals: one thread per interval (T.81 F.2.2.5: every RSTn resets the
+// streams with restart intervals: one lane per interval (T.81 F.2.2.5: every RSTn resets the
 // DC predictions and byte-aligns the bit stream, so intervals decode independently -- the
 // parallelism the reference's decoders never use, crates/zaru-image/src/jpeg.rs:107-205 and
 // TODO.txt:9-12).  The decode is runtime/jpeg.cpp's entropy_decode restated (same tables, same
@@ -15,167 +15,167 @@ constexpr uint8_t kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25,
                                  35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
                                  58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
-// the host Bits reader over one interval's bytes: 0xFF00 is a stuffed 0xFF, any other 0xFFxx (the
-// interval's RSTn / EOI) feeds zero bits from there on.  The bytes come through a window of
-// aligned 16-B words: `cur` is consumed, `nxt` only peeked at (a 0xFF at the end of `cur`) and
-// `far` is in flight -- issued one word before anything reads it, so no read waits on the load
-// just issued (a byte-serial reader is one dependent ~2 us global load per byte).
-struct DevBits {
-    const uint4 *base;  // the scan data (16-B aligned, >= 32 B of slack past the end)
-    int p, n;           // next byte, end of the interval
-    uint64_t acc;
-    int cnt;
-    bool marker;
-    int wb;             // byte offset of `cur`
-    uint4 cur, nxt, far;
-    __device__ void init(const uint8_t *data, int start, int end) {
-        base = reinterpret_cast<const uint4 *>(data);
-        p = start;
-        n = end;
-        acc = 0;
-        cnt = 0;
-        marker = false;
-        wb = start & ~15;
-        cur = base[wb >> 4];
-        nxt = base[(wb >> 4) + 1];
-        far = base[(wb >> 4) + 2];
+// The host unstuffs the scan while it copies it (0xFF00 -> 0xFF, each interval cut at its first
+// marker: runtime/jpeg.cpp unstuff_intervals), so an interval's bits are a plain byte range,
+// followed by zeros (the host reader's rule after a marker).  A workgroup (64 intervals, one per
+// lane) stages its contiguous range in LDS as big-endian dwords; a lane's 32-bit window at bit
+// `bp` is then a funnel shift of two register-cached dwords, and one window covers a whole
+// symbol (code <= 16 bits + magnitude <= 15 bits).  No refill loop, no per-byte branches: the earlier
+// byte-reader form of this kernel ran ~350 wave instructions per symbol.
+struct Window {
+    const uint32_t *w;  // the workgroup's staged dwords (big-endian)
+    int last;           // last dword index the reader may touch
+    int ebp;            // end of the lane's interval (bits)
+    int i;              // dword of the current bit position: hi = w[i], lo = w[i + 1], nx = w[i + 2]
+    uint32_t hi, lo, nx;
+    __device__ __forceinline__ void init(const uint32_t *words, int last_word, int bp, int end) {
+        w = words;
+        last = last_word;
+        ebp = end;
+        i = bp >> 5;
+        hi = w[min(i, last)];
+        lo = w[min(i + 1, last)];
+        nx = w[min(i + 2, last)];
     }
-    static __device__ __forceinline__ uint32_t byte_of(const uint4 &w, int o) {
-        const int k = o >> 2;
-        const uint32_t d = k == 0 ? w.x : k == 1 ? w.y : k == 2 ? w.z : w.w;
-        return (d >> ((o & 3) * 8)) & 0xFFu;
-    }
-    __device__ void fill() {
-        while (cnt <= 56) {
-            uint32_t b = 0;
-            if (!marker && p < n) {
-                if (p >= wb + 16) {  // slide the window; the load of the word after it starts now
-                    cur = nxt;
-                    nxt = far;
-                    wb += 16;
-                    far = base[(wb >> 4) + 2];
-                }
-                const int o = p - wb;
-                b = byte_of(cur, o);
-                if (b == 0xFF) {
-                    const uint32_t nx = p + 1 >= n ? 0xD9u : o < 15 ? byte_of(cur, o + 1) : nxt.x & 0xFFu;
-                    if (nx == 0x00) {
-                        p += 2;
-                    } else {
-                        marker = true;
-                        b = 0;
-                    }
-                } else {
-                    p++;
-                }
-            }
-            acc |= (uint64_t)b << (56 - cnt);
-            cnt += 8;
-        }
-    }
-    __device__ uint32_t peek(int k) {
-        if (cnt < k) fill();
-        return (uint32_t)(acc >> (64 - k));
-    }
-    __device__ void skip(int k) {
-        acc <<= k;
-        cnt -= k;
-    }
-    __device__ int get(int k) {
-        if (k == 0) return 0;
-        const uint32_t v = peek(k);
-        skip(k);
-        return (int)v;
+    // A symbol consumes at most 31 bits, so the position moves at most one dword per call.  `nx`
+    // is reloaded every call (no branch) and first read a call later: the LDS latency is off the
+    // per-symbol dependency chain, which is then one table lookup.
+    __device__ __forceinline__ uint32_t at(int bp) {
+        const bool sh = (bp >> 5) != i;
+        hi = sh ? lo : hi;
+        lo = sh ? nx : lo;
+        i += sh;
+        nx = w[min(i + 2, last)];
+        const int rem = ebp - bp, s = bp & 31;
+        const uint32_t v = s ? __builtin_amdgcn_alignbit(hi, lo, 32 - s) : hi;
+        return rem >= 32 ? v : rem <= 0 ? 0u : v & (~0u << (32 - rem));
     }
 };
 
-__device__ __forceinline__ int huff_decode(DevBits &b, const JpegHuffTable &h, bool &bad) {
-    const uint32_t l = b.peek(9);
-    const uint16_t e = h.look[l];
-    if (e) {
-        b.skip(e >> 8);
-        return e & 0xFF;
-    }
-    const uint32_t code = b.peek(16);
-    for (int len = 10; len <= 16; len++) {
-        const int32_t c = (int32_t)(code >> (16 - len));
-        if (c <= h.maxcode[len]) {
-            b.skip(len);
-            return h.vals[(c + h.valoff[len]) & 255];
+// A table's long-code limits in registers (uniform per block): the 10..16-bit search is seven
+// compares, not seven dependent LDS reads as in the host decoder's loop (runtime/jpeg.cpp decode).
+struct LongCodes {
+    uint32_t lim[7];
+    int32_t off[7];
+    __device__ __forceinline__ void load(const JpegHuffTable &t) {
+#pragma unroll
+        for (int j = 0; j < 7; j++) {
+            lim[j] = t.lim[j];
+            off[j] = t.off[j];
         }
     }
-    bad = true;
-    return 0;
-}
+    // symbol of the >= 10-bit code at the top of `win`; len = 0: no such code
+    __device__ __forceinline__ int decode(uint32_t win, const JpegHuffTable &t, int &len) const {
+        const uint32_t code = win >> 16;
+        int l = 0, o = 0;
+#pragma unroll
+        for (int j = 6; j >= 0; j--)
+            if (code < lim[j]) {
+                l = j + 10;
+                o = off[j];
+            }
+        len = l;
+        return l ? t.vals[((int)(code >> (16 - l)) + o) & 255] : 0;
+    }
+};
+
+// `s` bits of `win` after the first `len` (s >= 1, len + s <= 32)
+__device__ __forceinline__ int bits_after(uint32_t win, int len, int s) { return (int)((win << len) >> (32 - s)); }
 
 __device__ __forceinline__ int extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
 
-// Every coefficient goes to the thread's block in LDS (natural order through an LDS zig-zag
-// table) and the finished block leaves in eight 16-B stores: a zig-zag table in global memory
-// puts one dependent global load in front of every coefficient store (~2.5 us per symbol).
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x00010203u); }
+
+// Every coefficient goes to the lane's block in LDS (natural order through an LDS zig-zag table)
+// and the finished block leaves in eight 16-B stores.
 __global__ __launch_bounds__(64) void jpeg_huff_kernel(const JpegHuffParams P) {
     __shared__ JpegHuffTable T[8];
     __shared__ uint8_t zz[64];
-    __shared__ int4 sblk[64][8];  // one 64-coefficient int16 block per thread
-    {  // the tables, 16 B per thread-step
-        const uint4 *src = reinterpret_cast<const uint4 *>(P.tables);
+    __shared__ int4 sblk[64][8];  // one 64-coefficient int16 block per lane
+    extern __shared__ uint4 sdata[];
+    const JpegHuffFrame &F = P.frames[P.wg[2 * blockIdx.x]];
+    const int iv0 = P.wg[2 * blockIdx.x + 1], iv1 = min(iv0 + 64, F.n_iv);
+    const int a0 = F.iv_off[iv0] & ~15;
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(F.tables);
         uint4 *dst = reinterpret_cast<uint4 *>(T);
         constexpr int n16 = (int)(8 * sizeof(JpegHuffTable) / 16);
         for (int i = threadIdx.x; i < n16; i += 64) dst[i] = src[i];
         zz[threadIdx.x] = kZigzag[threadIdx.x];
+        // the range + one look-ahead word (the device buffer has >= 32 B of slack past the end)
+        const int n16d = (F.iv_off[iv1] - a0 + 15) / 16 + 1;
+        const uint4 *d = reinterpret_cast<const uint4 *>(F.data + a0);
+        for (int i = threadIdx.x; i < n16d; i += 256) {
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (i + 64 * u < n16d) v[u] = d[i + 64 * u];
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (i + 64 * u < n16d)
+                    sdata[i + 64 * u] = make_uint4(bswap32(v[u].x), bswap32(v[u].y), bswap32(v[u].z), bswap32(v[u].w));
+        }
     }
     __syncthreads();
+    const int iv = iv0 + threadIdx.x;
+    if (iv >= iv1) return;
+    int bp = (F.iv_off[iv] - a0) * 8;
+    Window win;
+    win.init(reinterpret_cast<const uint32_t *>(sdata), ((F.iv_off[iv1] - a0 + 15) / 16 + 1) * 4 - 1, bp,
+             (F.iv_off[iv + 1] - a0) * 8);
     int4 *const mine = sblk[threadIdx.x];
     int16_t *const co = reinterpret_cast<int16_t *>(mine);
-    const int iv = blockIdx.x * 64 + threadIdx.x;
-    if (iv >= P.n_iv) return;
-    DevBits bits;
-    bits.init(P.data, P.iv_off[iv], P.iv_off[iv + 1]);
     int pred[3] = {0, 0, 0};
     bool bad = false;
-    const int m0 = iv * P.restart, m1 = min(m0 + P.restart, P.nmcu);
+    const int m0 = iv * F.restart, m1 = min(m0 + F.restart, F.nmcu);
     for (int m = m0; m < m1 && !bad; m++) {
-        const int my = m / P.mcux, mx = m - my * P.mcux;
-        for (int c = 0; c < P.ncomp; c++) {
-            const JpegHuffTable &dc = T[P.td[c]], &ac = T[4 + P.ta[c]];
-            for (int v = 0; v < P.cv[c]; v++)
-                for (int h = 0; h < P.ch[c]; h++) {
-                    const int by = my * P.cv[c] + v, bx = mx * P.ch[c] + h;
+        const int my = m / F.mcux, mx = m - my * F.mcux;
+        for (int c = 0; c < F.ncomp; c++) {
+            const JpegHuffTable &dc = T[F.td[c]], &ac = T[4 + F.ta[c]];
+            LongCodes dcl, acl;
+            dcl.load(dc);
+            acl.load(ac);
+            for (int v = 0; v < F.cv[c]; v++)
+                for (int h = 0; h < F.ch[c]; h++) {
+                    const int by = my * F.cv[c] + v, bx = mx * F.ch[c] + h;
                     int4 *const b4 = reinterpret_cast<int4 *>(
-                        P.coef + (P.coef_off[c] + (int64_t)by * P.bw[c] + bx) * 64);
+                        F.coef + (F.coef_off[c] + (int64_t)by * F.bw[c] + bx) * 64);
 #pragma unroll
                     for (int z = 0; z < 8; z++) mine[z] = make_int4(0, 0, 0, 0);
-                    const int s = huff_decode(bits, dc, bad);
-                    if (s > 11) bad = true;
-                    pred[c] += s && s <= 11 ? extend(bits.get(s), s) : 0;
-                    co[0] = (int16_t)pred[c];
-                    for (int k = 1; k < 64 && !bad;) {
-                        const int fa = ac.fast_ac[bits.peek(9)];
-                        if (fa) {  // run, size and magnitude in one lookup
-                            k += (fa >> 4) & 15;
-                            bits.skip(fa & 15);
-                            if (k > 63) {
-                                bad = true;
-                                break;
-                            }
-                            co[zz[k]] = (int16_t)(fa >> 8);
-                            k++;
-                            continue;
-                        }
-                        const int rs = huff_decode(bits, ac, bad);
+                    {  // DC: category, then that many magnitude bits
+                        const uint32_t w = win.at(bp);
+                        const uint32_t e = dc.lk[w >> 23] & 0xFFFFu;
+                        int ll;
+                        const int slow = dcl.decode(w, dc, ll);
+                        const int len = e ? (int)(e >> 8) : ll;
+                        const int sc = e ? (int)(e & 0xFF) : slow;
+                        const bool ok = len && sc <= 11;
+                        bad |= !ok;
+                        pred[c] += ok && sc ? extend(bits_after(w, len, sc), sc) : 0;
+                        bp += len + (ok ? sc : 0);
+                        co[0] = (int16_t)pred[c];
+                    }
+                    // AC, branch-free per symbol (lanes decode different data, so every branch
+                    // would be taken by some lane): the fast entry and the long-code search are
+                    // both evaluated and selected
+                    for (int k = bad ? 64 : 1; k < 64;) {
+                        const uint32_t w = win.at(bp);
+                        const uint32_t e = ac.lk[w >> 23];
+                        int ll;
+                        const int slow = acl.decode(w, ac, ll);
+                        const int fa = (int32_t)e >> 16;
+                        const bool f = fa != 0, look = (e & 0xFFFFu) != 0;
+                        const int len = look ? (int)((e >> 8) & 0xFF) : ll;
+                        const int rs = look ? (int)(e & 0xFF) : slow;
                         const int r = rs >> 4, sz = rs & 15;
-                        if (sz) {
-                            k += r;
-                            if (k > 63) {
-                                bad = true;
-                                break;
-                            }
-                            co[zz[k]] = (int16_t)extend(bits.get(sz), sz);
-                            k++;
-                        } else {
-                            if (r != 15) break;
-                            k += 16;
-                        }
+                        const bool coef = f || sz;  // writes a coefficient (else EOB / ZRL)
+                        const int kn = k + (f ? (fa >> 4) & 15 : r);
+                        const bool bad_now = (!f && !len) || (coef && kn > 63);
+                        const int val = f ? fa >> 8 : sz ? extend(bits_after(w, len, sz), sz) : 0;
+                        if (coef && !bad_now) co[zz[kn & 63]] = (int16_t)val;
+                        bp += f ? fa & 15 : len + sz;
+                        k = bad_now ? 64 : coef ? kn + 1 : r == 15 ? k + 16 : 64;
+                        bad |= bad_now;
                     }
 #pragma unroll
                     for (int z = 0; z < 8; z++) b4[z] = mine[z];
@@ -187,8 +187,15 @@ __global__ __launch_bounds__(64) void jpeg_huff_kernel(const JpegHuffParams P) {
 
 }  // namespace
 
+int jpeg_huff_max_lds() { return 160 * 1024 - (int)(8 * sizeof(JpegHuffTable) + 64 + 64 * 128) - 1024; }
+
 const char *launch_jpeg_huff(const JpegHuffParams &p, hipStream_t s) {
-    hipLaunchKernelGGL(jpeg_huff_kernel, dim3((p.n_iv + 63) / 64), dim3(64), 0, s, p);
+    static const bool attr = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void *>(jpeg_huff_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, jpeg_huff_max_lds()) == hipSuccess;
+    }();
+    (void)attr;
+    hipLaunchKernelGGL(jpeg_huff_kernel, dim3(p.n_wg), dim3(64), (size_t)p.lds_bytes, s, p);
     return "jpeg_huff_kernel";
 }
 

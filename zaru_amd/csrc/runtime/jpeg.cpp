@@ -373,39 +373,56 @@ void entropy_decode(const Header &hd, const zr::JpegParams &P, const uint8_t *jp
 void dev_table(const Huff &h, zr::JpegHuffTable &t) {
     std::memset(&t, 0, sizeof t);
     if (!h.present) return;
-    std::memcpy(t.look, h.look, sizeof t.look);
-    std::memcpy(t.fast_ac, h.fast_ac, sizeof t.fast_ac);
-    std::memcpy(t.maxcode, h.maxcode, sizeof t.maxcode);
-    std::memcpy(t.valoff, h.valoff, sizeof t.valoff);
+    for (int i = 0; i < 512; i++) t.lk[i] = ((uint32_t)(uint16_t)h.fast_ac[i] << 16) | h.look[i];
+    // code >> (16 - l) <= maxcode[l]  <=>  code < (maxcode[l] + 1) << (16 - l): decode()'s test
+    for (int l = 10; l <= 16; l++) {
+        t.lim[l - 10] = (uint32_t)(h.maxcode[l] + 1) << (16 - l);
+        t.off[l - 10] = h.valoff[l];
+    }
     std::memcpy(t.vals, h.vals, sizeof t.vals);
 }
 
-// Byte offsets (from scan_begin) where each restart interval's entropy-coded data starts, plus the
-// end of the scan (the EOI / first non-RST marker); false when the stream does not have exactly
-// one interval per `restart` MCUs -- the caller then decodes on the host, which reports errors.
-bool restart_intervals(const uint8_t *d, size_t n, size_t begin, int n_iv, std::vector<int32_t> &off) {
+// The scan's restart intervals, unstuffed and back to back in `out` (which has room for the scan):
+// interval i is out[off[i], off[i+1]).  Each interval is cut at its first marker -- a 0xFF not
+// followed by 0x00, so a fill byte or the RSTn itself -- since the host reader (Bits) feeds zeros
+// from there; its next interval starts after the next RSTn, where Bits::restart() resumes.  False
+// when the stream does not have exactly one interval per `restart` MCUs (the caller then decodes
+// on the host, which reports the errors).
+bool unstuff_intervals(const uint8_t *d, size_t n, size_t begin, int n_iv, uint8_t *out, std::vector<int32_t> &off) {
     off.clear();
     off.push_back(0);
-    size_t p = begin;
-    while (p + 1 < n) {
-        const uint8_t *f = static_cast<const uint8_t *>(std::memchr(d + p, 0xFF, n - 1 - p));
-        if (!f) break;
-        p = (size_t)(f - d);
-        const uint8_t nx = d[p + 1];
-        if (nx == 0x00 || nx == 0xFF) {  // stuffed byte / fill byte
-            p += nx == 0x00 ? 2 : 1;
-            continue;
+    size_t p = begin, o = 0;
+    bool open = true;  // the current interval still takes bytes
+    while (p < n) {
+        const uint8_t *f = static_cast<const uint8_t *>(std::memchr(d + p, 0xFF, n - p));
+        const size_t q = f ? (size_t)(f - d) : n;
+        if (open) {
+            std::memcpy(out + o, d + p, q - p);
+            o += q - p;
         }
-        if (nx >= 0xD0 && nx <= 0xD7) {
-            off.push_back((int32_t)(p + 2 - begin));
-            p += 2;
-            continue;
+        if (q + 1 >= n) {  // no marker left (a trailing 0xFF reads as one: Bits' 0xD9 rule)
+            p = n;
+            break;
         }
-        break;  // EOI or another marker ends the scan
+        const uint8_t nx = d[q + 1];
+        if (nx == 0x00) {  // stuffed 0xFF
+            if (open) out[o++] = 0xFF;
+            p = q + 2;
+        } else if (nx == 0xFF) {  // fill byte: Bits stops here, restart() looks for the RSTn
+            open = false;
+            p = q + 1;
+        } else if (nx >= 0xD0 && nx <= 0xD7) {
+            if (o >= ((size_t)1 << 31)) return false;
+            off.push_back((int32_t)o);
+            open = true;
+            p = q + 2;
+        } else {
+            break;  // EOI or another marker ends the scan
+        }
     }
-    const size_t end = p + 1 < n ? p : n;
-    off.push_back((int32_t)(end - begin));
-    return (int)off.size() == n_iv + 1 && end - begin < ((size_t)1 << 31);
+    if (o >= ((size_t)1 << 31)) return false;
+    off.push_back((int32_t)o);
+    return (int)off.size() == n_iv + 1;
 }
 
 bool gpu_entropy_enabled() {  // ZARU_JPEG_HOST_ENTROPY=1 keeps every decode on the host (A/B)
@@ -532,23 +549,63 @@ int zr_jpeg_coefficients(const uint8_t *jpeg, size_t len, int16_t *coef, size_t 
 
 int zr_jpeg_decode_async(zr_jpeg_decoder *dec, const uint8_t *jpeg, size_t len, uint8_t *d_rgba,
                          size_t row_stride, void *hip_stream) {
+    return zr_jpeg_decode_batch_async(dec, 1, &jpeg, &len, &d_rgba, &row_stride, hip_stream);
+}
+
+int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *const *jpegs, const size_t *lens,
+                               uint8_t *const *d_rgba, const size_t *row_strides, void *hip_stream) {
     try {
-        if (!dec || !jpeg || !d_rgba) return err(ZR_ERR_INVALID_ARGUMENT, "null argument");
+        if (!dec || !jpegs || !lens || !d_rgba || !row_strides) return err(ZR_ERR_INVALID_ARGUMENT, "null argument");
+        if (n == 0) return ZR_OK;
+        if (n > 4096) return err(ZR_ERR_INVALID_ARGUMENT, "jpeg: batch larger than 4096 frames");
         std::lock_guard<std::mutex> g(dec->mu);
-        Header hd;
-        parse(jpeg, len, hd);
-        if (row_stride < (size_t)hd.W * 4) return err(ZR_ERR_INVALID_ARGUMENT, "row_stride < 4*width");
-        zr::JpegParams P;
-        layout_of(hd, P);
-        const int64_t blocks = P.total_blocks;
-        const int64_t pbytes = blocks * 64;
-        // stage the coefficients: the previous decode's copy out of the staging must be done
+        // every frame parsed and checked before anything is enqueued
+        std::vector<Header> hd(n);
+        std::vector<zr::JpegParams> P(n);
+        std::vector<int64_t> cofs(n);  // block offset of each frame's coefficients in d_coef
+        int64_t blocks = 0, pbytes = 0;
+        for (size_t f = 0; f < n; f++) {
+            if (!jpegs[f] || !d_rgba[f]) return err(ZR_ERR_INVALID_ARGUMENT, "null argument");
+            try {
+                parse(jpegs[f], lens[f], hd[f]);
+                layout_of(hd[f], P[f]);
+            } catch (const JpegError &e) {
+                return err(e.code, n > 1 ? e.msg + " (frame " + std::to_string(f) + ")" : e.msg);
+            }
+            if (row_strides[f] < (size_t)hd[f].W * 4) return err(ZR_ERR_INVALID_ARGUMENT, "row_stride < 4*width");
+            cofs[f] = blocks;
+            blocks += P[f].total_blocks;
+            pbytes = std::max(pbytes, (int64_t)P[f].total_blocks * 64);
+        }
+        // the previous decode's copies out of the staging buffers must be done
         if (hipSetDevice(dec->device) != hipSuccess) return err(ZR_ERR_DEVICE, "hipSetDevice failed");
         if (hipEventSynchronize(dec->staged) != hipSuccess) return err(ZR_ERR_DEVICE, "event sync failed");
-        // growing frees the device buffers: the previous decode's kernels must be done with them
-        if (((size_t)blocks > dec->coef_cap || (size_t)pbytes > dec->planes_cap) &&
-            hipEventSynchronize(dec->done) != hipSuccess)
-            return err(ZR_ERR_DEVICE, "event sync failed");
+        // which frames decode their entropy on the device, and the staging they need at most:
+        // [frames][wg list][per frame: 8 tables, interval offsets, unstuffed intervals + look-ahead]
+        const size_t tb = 8 * sizeof(zr::JpegHuffTable);
+        std::vector<int> n_iv(n, 0), mcux(n, 0), nmcu(n, 0);
+        std::vector<size_t> ob(n, 0), fofs(n, 0);
+        size_t groups = 0, stage = 0;
+        for (size_t f = 0; f < n; f++) {
+            mcux[f] = P[f].bw[0] / hd[f].comp[0].h;
+            nmcu[f] = mcux[f] * (P[f].bh[0] / hd[f].comp[0].v);
+            n_iv[f] = hd[f].restart > 0 ? (nmcu[f] + hd[f].restart - 1) / hd[f].restart : 0;
+            if (!gpu_entropy_enabled() || n_iv[f] < 8) n_iv[f] = 0;
+            if (!n_iv[f]) continue;
+            ob[f] = ((size_t)(n_iv[f] + 1) * 4 + 15) / 16 * 16;
+            groups += (size_t)(n_iv[f] + 63) / 64;
+        }
+        const size_t fb = (n * sizeof(zr::JpegHuffFrame) + 15) / 16 * 16, wb = (groups * 8 + 15) / 16 * 16;
+        stage = fb + wb;
+        for (size_t f = 0; f < n; f++)
+            if (n_iv[f]) {
+                fofs[f] = stage;
+                stage += tb + ob[f] + ((lens[f] - hd[f].scan_begin) + 48 + 15) / 16 * 16;
+            }
+        // growing frees device buffers: the previous decode's kernels must be done with them
+        const bool grow = (size_t)blocks > dec->coef_cap || (size_t)pbytes > dec->planes_cap ||
+                          (groups && stage > dec->stage_cap);
+        if (grow && hipEventSynchronize(dec->done) != hipSuccess) return err(ZR_ERR_DEVICE, "event sync failed");
         if ((size_t)blocks > dec->coef_cap) {
             (void)hipHostFree(dec->h_coef);
             (void)hipFree(dec->d_coef);
@@ -569,74 +626,117 @@ int zr_jpeg_decode_async(zr_jpeg_decoder *dec, const uint8_t *jpeg, size_t len, 
             if (hipMalloc((void **)&dec->d_planes, cap) != hipSuccess) return err(ZR_ERR_DEVICE, "jpeg: out of memory");
             dec->planes_cap = cap;
         }
-        hipStream_t st = (hipStream_t)hip_stream;
-        const int mcux = P.bw[0] / hd.comp[0].h, nmcu = mcux * (P.bh[0] / hd.comp[0].v);
-        const int n_iv = hd.restart > 0 ? (nmcu + hd.restart - 1) / hd.restart : 0;
-        std::vector<int32_t> ivo;
-        if (gpu_entropy_enabled() && n_iv >= 8 && restart_intervals(jpeg, len, hd.scan_begin, n_iv, ivo)) {
-            // device entropy decoding: [8 tables][interval offsets][scan bytes] in one copy
-            const size_t tb = 8 * sizeof(zr::JpegHuffTable), ob = ((size_t)(n_iv + 1) * 4 + 15) / 16 * 16;
-            const size_t db = (size_t)ivo.back(), need = tb + ob + db + 48;  // + the reader's look-ahead words
-            if (need > dec->stage_cap) {
-                if (hipEventSynchronize(dec->done) != hipSuccess) return err(ZR_ERR_DEVICE, "event sync failed");
-                (void)hipHostFree(dec->h_stage);
-                (void)hipFree(dec->d_stage);
-                dec->h_stage = nullptr;
-                dec->d_stage = nullptr;
-                dec->stage_cap = 0;
-                const size_t cap = need + need / 4;
-                if (hipHostMalloc((void **)&dec->h_stage, cap) != hipSuccess ||
-                    hipMalloc((void **)&dec->d_stage, cap) != hipSuccess)
-                    return err(ZR_ERR_DEVICE, "jpeg: out of memory");
-                dec->stage_cap = cap;
-            }
-            auto *tabs = reinterpret_cast<zr::JpegHuffTable *>(dec->h_stage);
-            for (int t = 0; t < 4; t++) {
-                dev_table(hd.dc[t], tabs[t]);
-                dev_table(hd.ac[t], tabs[4 + t]);
-            }
-            std::memcpy(dec->h_stage + tb, ivo.data(), (size_t)(n_iv + 1) * 4);
-            std::memcpy(dec->h_stage + tb + ob, jpeg + hd.scan_begin, db);
-            if (hipStreamWaitEvent(st, dec->done, 0) != hipSuccess ||
-                hipMemcpyAsync(dec->d_stage, dec->h_stage, need, hipMemcpyHostToDevice, st) != hipSuccess ||
-                hipEventRecord(dec->staged, st) != hipSuccess)
-                return err(ZR_ERR_DEVICE, "jpeg: scan upload failed");
-            zr::JpegHuffParams hp{};
-            hp.tables = reinterpret_cast<const zr::JpegHuffTable *>(dec->d_stage);
-            hp.iv_off = reinterpret_cast<const int32_t *>(dec->d_stage + tb);
-            hp.data = dec->d_stage + tb + ob;
-            hp.coef = dec->d_coef;
-            hp.n_iv = n_iv;
-            hp.restart = hd.restart;
-            hp.nmcu = nmcu;
-            hp.mcux = mcux;
-            hp.ncomp = hd.ncomp;
-            for (int c = 0; c < hd.ncomp; c++) {
-                hp.ch[c] = hd.comp[c].h;
-                hp.cv[c] = hd.comp[c].v;
-                hp.td[c] = hd.comp[c].td;
-                hp.ta[c] = hd.comp[c].ta;
-                hp.coef_off[c] = P.coef_off[c];
-                hp.bw[c] = P.bw[c];
-            }
-            hp.error = dec->d_err;
-            zr::launch_jpeg_huff(hp, st);
-            dec->n_gpu++;
-        } else {
-            entropy_decode(hd, P, jpeg, len, dec->h_coef);
-            // d_coef / d_planes are reused: on another stream the previous decode's IDCT and
-            // colour kernels may still read them, so this stream waits for them first
-            if (hipStreamWaitEvent(st, dec->done, 0) != hipSuccess ||
-                hipMemcpyAsync(dec->d_coef, dec->h_coef, (size_t)blocks * 128, hipMemcpyHostToDevice, st) != hipSuccess ||
-                hipEventRecord(dec->staged, st) != hipSuccess)
-                return err(ZR_ERR_DEVICE, "jpeg: coefficient upload failed");
-            dec->n_host++;
+        if (groups && stage > dec->stage_cap) {
+            (void)hipHostFree(dec->h_stage);
+            (void)hipFree(dec->d_stage);
+            dec->h_stage = nullptr;
+            dec->d_stage = nullptr;
+            dec->stage_cap = 0;
+            const size_t cap = stage + stage / 4;
+            if (hipHostMalloc((void **)&dec->h_stage, cap) != hipSuccess ||
+                hipMalloc((void **)&dec->d_stage, cap) != hipSuccess)
+                return err(ZR_ERR_DEVICE, "jpeg: out of memory");
+            dec->stage_cap = cap;
         }
-        P.coef = dec->d_coef;
-        P.planes = dec->d_planes;
-        P.out = d_rgba;
-        P.out_stride = (int64_t)row_stride;
-        zr::launch_jpeg(P, st);
+        // unstuff the device frames' scans; a frame whose intervals do not match its DRI, or whose
+        // 64-interval ranges exceed a workgroup's LDS, goes to the host path
+        std::vector<int32_t> ivo;
+        int lds = 0;
+        auto *fr = reinterpret_cast<zr::JpegHuffFrame *>(dec->h_stage);
+        auto *wg = reinterpret_cast<int32_t *>(dec->h_stage + fb);
+        size_t n_wg = 0, used = fb + wb;
+        for (size_t f = 0; f < n; f++) {
+            if (!n_iv[f]) continue;
+            uint8_t *const base = dec->h_stage + fofs[f];
+            if (!unstuff_intervals(jpegs[f], lens[f], hd[f].scan_begin, n_iv[f], base + tb + ob[f], ivo)) {
+                n_iv[f] = 0;
+                continue;
+            }
+            int need = 0;
+            for (int g0 = 0; g0 < n_iv[f]; g0 += 64) {
+                const int r = ivo[std::min(g0 + 64, n_iv[f])] - (ivo[g0] & ~15);
+                need = std::max(need, ((r + 15) / 16 + 1) * 16);
+            }
+            if (need > zr::jpeg_huff_max_lds()) {
+                n_iv[f] = 0;
+                continue;
+            }
+            lds = std::max(lds, need);
+            const size_t db = (size_t)ivo.back();
+            auto *tabs = reinterpret_cast<zr::JpegHuffTable *>(base);
+            for (int t = 0; t < 4; t++) {
+                dev_table(hd[f].dc[t], tabs[t]);
+                dev_table(hd[f].ac[t], tabs[4 + t]);
+            }
+            std::memcpy(base + tb, ivo.data(), (size_t)(n_iv[f] + 1) * 4);
+            std::memset(base + tb + ob[f] + db, 0, 48);
+            uint8_t *const dbase = dec->d_stage + fofs[f];
+            zr::JpegHuffFrame &F = fr[f];
+            F = zr::JpegHuffFrame{};
+            F.tables = reinterpret_cast<const zr::JpegHuffTable *>(dbase);
+            F.iv_off = reinterpret_cast<const int32_t *>(dbase + tb);
+            F.data = dbase + tb + ob[f];
+            F.coef = dec->d_coef + cofs[f] * 64;
+            F.n_iv = n_iv[f];
+            F.restart = hd[f].restart;
+            F.nmcu = nmcu[f];
+            F.mcux = mcux[f];
+            F.ncomp = hd[f].ncomp;
+            for (int c = 0; c < hd[f].ncomp; c++) {
+                F.ch[c] = hd[f].comp[c].h;
+                F.cv[c] = hd[f].comp[c].v;
+                F.td[c] = hd[f].comp[c].td;
+                F.ta[c] = hd[f].comp[c].ta;
+                F.coef_off[c] = P[f].coef_off[c];
+                F.bw[c] = P[f].bw[c];
+            }
+            for (int g0 = 0; g0 < n_iv[f]; g0 += 64) {
+                wg[2 * n_wg] = (int32_t)f;
+                wg[2 * n_wg + 1] = g0;
+                n_wg++;
+            }
+            used = fofs[f] + tb + ob[f] + (db + 48 + 15) / 16 * 16;
+        }
+        // host entropy decoding for the rest, into their slots of the pinned coefficient staging
+        for (size_t f = 0; f < n; f++)
+            if (!n_iv[f]) {
+                try {
+                    entropy_decode(hd[f], P[f], jpegs[f], lens[f], dec->h_coef + cofs[f] * 64);
+                } catch (const JpegError &e) {
+                    return err(e.code, n > 1 ? e.msg + " (frame " + std::to_string(f) + ")" : e.msg);
+                }
+            }
+        // d_coef / d_planes / d_stage are reused: on another stream the previous decode's kernels
+        // may still read them, so this stream waits for them first
+        hipStream_t st = (hipStream_t)hip_stream;
+        if (hipStreamWaitEvent(st, dec->done, 0) != hipSuccess) return err(ZR_ERR_DEVICE, "jpeg: stream wait failed");
+        for (size_t f = 0; f < n; f++)
+            if (!n_iv[f] && hipMemcpyAsync(dec->d_coef + cofs[f] * 64, dec->h_coef + cofs[f] * 64,
+                                           (size_t)P[f].total_blocks * 128, hipMemcpyHostToDevice, st) != hipSuccess)
+                return err(ZR_ERR_DEVICE, "jpeg: coefficient upload failed");
+        if (n_wg && hipMemcpyAsync(dec->d_stage, dec->h_stage, used, hipMemcpyHostToDevice, st) != hipSuccess)
+            return err(ZR_ERR_DEVICE, "jpeg: scan upload failed");
+        if (hipEventRecord(dec->staged, st) != hipSuccess) return err(ZR_ERR_DEVICE, "jpeg: event record failed");
+        if (n_wg) {
+            zr::JpegHuffParams hp{};
+            hp.frames = reinterpret_cast<const zr::JpegHuffFrame *>(dec->d_stage);
+            hp.wg = reinterpret_cast<const int32_t *>(dec->d_stage + fb);
+            hp.n_wg = (int)n_wg;
+            hp.error = dec->d_err;
+            hp.lds_bytes = lds;
+            zr::launch_jpeg_huff(hp, st);
+        }
+        for (size_t f = 0; f < n; f++) {
+            P[f].coef = dec->d_coef + cofs[f] * 64;
+            P[f].planes = dec->d_planes;
+            P[f].out = d_rgba[f];
+            P[f].out_stride = (int64_t)row_strides[f];
+            zr::launch_jpeg(P[f], st);
+            if (n_iv[f])
+                dec->n_gpu++;
+            else
+                dec->n_host++;
+        }
         if (hipGetLastError() != hipSuccess || hipEventRecord(dec->done, st) != hipSuccess)
             return err(ZR_ERR_DEVICE, "jpeg: kernel launch failed");
         return ZR_OK;

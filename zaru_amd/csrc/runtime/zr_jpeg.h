@@ -2,7 +2,7 @@
 // inverse DCT per 8x8 block, then upsampling + YCbCr -> RGBA per output pixel, restating the
 // reference's libjpeg-turbo backend (crates/zaru-image/src/jpeg.rs:164-182: turbojpeg 0.5.3 /
 // turbojpeg-sys 0.2.3, default flags: accurate integer IDCT "islow", fancy upsampling).  The
-// entropy decoding runs on the device for streams with restart intervals (one thread per
+// entropy decoding runs on the device for streams with restart intervals (one lane per
 // interval, jpeg_huff.hip) and on the host otherwise (runtime/jpeg.cpp).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -35,26 +35,35 @@ const char *launch_jpeg(const JpegParams &p, hipStream_t s);
 // the bit stream is byte-aligned at every RSTn), so one thread decodes one interval.  Tables in
 // the host decoder's form (runtime/jpeg.cpp Huff), copied with the scan data.
 struct JpegHuffTable {
-    uint16_t look[512];    // 9-bit lookahead: (length << 8) | symbol, 0 = longer code
-    int16_t fast_ac[512];  // AC: (value << 8) | (run << 4) | total bits, 0 = slow path
-    int32_t maxcode[18];
-    int32_t valoff[17];
+    uint32_t lk[512];  // 9-bit lookahead: (fast_ac << 16) | look -- look = (length << 8) | symbol,
+                       // 0 = longer code; fast_ac = (value << 8) | (run << 4) | total bits, 0 = none
+    uint32_t lim[8];   // codes of 10..16 bits: [l - 10] = (maxcode[l] + 1) << (16 - l), 0 = none
+    int32_t off[8];    // [l - 10] = valoff[l]
     uint8_t vals[256];
-    uint8_t pad_[4];
 };
 static_assert(sizeof(JpegHuffTable) % 16 == 0, "JpegHuffTable is copied as 16-byte slots");
 
-struct JpegHuffParams {
+struct JpegHuffFrame {
     const JpegHuffTable *tables;  // [8]: DC 0..3, AC 0..3
     const int32_t *iv_off;        // [n_iv + 1] byte offsets of the intervals in `data` (+ end)
-    const uint8_t *data;          // the scan's entropy-coded bytes (RSTn markers included)
+    const uint8_t *data;          // the intervals' unstuffed bytes, back to back (16-B aligned)
     int16_t *coef;                // as JpegParams::coef
+    int64_t coef_off[3];
     int n_iv, restart, nmcu, mcux, ncomp;
     int ch[3], cv[3], td[3], ta[3];
-    int64_t coef_off[3];
     int bw[3];
-    int *error;                   // set to 1 on a corrupt interval (bad code / AC index)
 };
+
+// One launch decodes a batch of frames: workgroup w takes frame wg[2w]'s 64 intervals from
+// wg[2w + 1] on.
+struct JpegHuffParams {
+    const JpegHuffFrame *frames;
+    const int32_t *wg;            // [n_wg][2]
+    int n_wg;
+    int *error;                   // set to 1 on a corrupt interval (bad code / AC index)
+    int lds_bytes;                // dynamic LDS: the largest 64-interval range, 16-B words + 1
+};
+int jpeg_huff_max_lds();          // the most dynamic LDS one workgroup may stage
 const char *launch_jpeg_huff(const JpegHuffParams &p, hipStream_t s);
 
 }  // namespace zr

@@ -62,6 +62,19 @@ class JpegDecoder:
         `row_stride` bytes) on `stream` (default stream when None)."""
         check(lib().zr_jpeg_decode_async(self._h, data, len(data), d_rgba, row_stride, stream))
 
+    def decode_batch_into(self, datas, d_rgba, row_strides, stream=None):
+        """Enqueue the decodes of the byte strings `datas` into the device buffers `d_rgba[i]`
+        (RGBA8 rows of `row_strides[i]` bytes) on `stream`: one Huffman launch for all frames
+        that decode on the device (zr_jpeg_decode_batch_async)."""
+        n = len(datas)
+        if not (len(d_rgba) == len(row_strides) == n):
+            raise ValueError("datas, d_rgba and row_strides differ in length")
+        bufs = (C.c_char_p * n)(*datas)
+        lens = (C.c_size_t * n)(*[len(d) for d in datas])
+        outs = (C.c_void_p * n)(*d_rgba)
+        strides = (C.c_size_t * n)(*row_strides)
+        check(lib().zr_jpeg_decode_batch_async(self._h, n, bufs, lens, outs, strides, stream))
+
     def status(self):
         """(device entropy decodes, host entropy decodes, corrupt flag) since creation."""
         g, h, c = C.c_uint64(), C.c_uint64(), C.c_int()
