@@ -296,3 +296,48 @@ def test_batch_decode_rejects_a_bad_frame_before_enqueueing(dec):
             assert np.array_equal(got[i], want)
     finally:
         d.close()
+
+
+def test_unaligned_output_and_odd_row_stride(dec):
+    """The ABI asks only row_stride >= 4 * width: a frame buffer at an odd address with an odd
+    stride takes the byte-store path of the colour stage and must hold the same pixels."""
+    from zaru_amd._lib import DeviceBuffer, lib
+    h, w = 37, 53
+    data = encode(synthetic(h, w, 12), quality=90, restart_marker_blocks=1)
+    stride = w * 4 + 3
+    buf = DeviceBuffer(h * stride + 8)
+    dec.decode_into(data, buf.ptr + 1, stride)
+    lib().zr_stream_synchronize(None)
+    raw = buf.download((h * stride + 8,), "uint8")
+    got = np.stack([raw[1 + r * stride:1 + r * stride + w * 4].reshape(w, 4) for r in range(h)])
+    assert np.array_equal(got, libjpeg_turbo_rgba(data))
+
+
+def _with_quant(data, value):
+    """The stream with every quantisation table entry set to `value` (8-bit tables)."""
+    b = bytearray(data)
+    i = 2
+    while i + 4 <= len(b) and b[i] == 0xFF and b[i + 1] != 0xDA:
+        seg = int.from_bytes(b[i + 2:i + 4], "big")
+        if b[i + 1] == 0xDB:
+            j = i + 4
+            while j < i + 2 + seg:
+                assert b[j] >> 4 == 0
+                b[j + 1:j + 65] = bytes([value]) * 64
+                j += 65
+        i += 2 + seg
+    return bytes(b)
+
+
+@pytest.mark.parametrize("kw", [{}, {"restart_marker_blocks": 2}])
+def test_out_of_range_coefficients_take_the_wide_idct(dec, kw):
+    """A quality-100 stream re-labelled with all-255 quantisation tables dequantises past 2^15
+    (no legal encoder output does): jpeg_idct_kernel's blocks fall back from int32 to 64-bit
+    arithmetic, libjpeg-turbo's JLONG islow.  Checked against the oracle's 64-bit islow
+    (oracle/jpeg.c) over the host decoder's coefficients of the same stream."""
+    import oracle as O
+    from zaru_amd import jpeg
+    data = _with_quant(encode(synthetic(96, 128, 21), quality=100, **kw), 255)
+    layout, coef = jpeg.coefficients(data)
+    assert np.abs(coef.astype(np.int64) * 255).max() >= 1 << 15
+    assert np.array_equal(dec.decode(data), O.jpeg_pixels(coef, layout))
