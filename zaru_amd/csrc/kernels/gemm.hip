@@ -93,6 +93,38 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmParams P) {
     for (int t = 0; t < MT; ++t) epilogue_tile(P, acc[t], n, q, m0 + t * 32, kh);
 }
 
+// Small-K form of gemm_kernel<1, false> (K <= NCH * 32, M <= 32: the FaceMesh tail's 128 -> 32
+// 1x1 convs over batch x 3x3 columns that the LDS-tiled form cannot take, ncols % 4 != 0).  Every
+// operand of the whole K extent is loaded up front in straight-line code (the weights straight
+// from global memory: 16 KB, L2-resident), so the launch costs one load latency instead of one
+// per chunk (gemm_kernel stages each chunk through LDS behind two barriers).  The MFMA sequence
+// is gemm_kernel's, operand for operand, so the bits are too.
+template <int NCH>
+__global__ __launch_bounds__(256) void gemm_smallk_kernel(const GemmParams P) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int kh = lane >> 5, col = lane & 31;
+    const int j = (blockIdx.x * 4 + wave) * 32 + col;
+    const bool valid = j < P.ncols;
+    const int jj = valid ? j : 0;
+    const int n = jj / P.P, q = jj - n * P.P;
+    const float *xc = P.x + (int64_t)n * P.x_sN + q;
+    float a[NCH * KC / 2], b[NCH * KC / 2];
+#pragma unroll
+    for (int s = 0; s < NCH * KC / 2; ++s) {
+        const int k = 2 * s + kh;
+        a[s] = k < P.Kpad && col < P.Mpad ? P.wt[(int64_t)(k < P.Kpad ? k : 0) * P.Mpad + col] : 0.f;
+        const float v = xc[(int64_t)(k < P.K ? k : P.K - 1) * P.x_sC];
+        b[s] = k < P.K ? v : 0.f;
+    }
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < NCH * KC / 2; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+    if (!valid) return;
+    epilogue_tile(P, acc, n, q, 0, kh);
+}
+
 // ---------------------------------------------------------------- LDS-tiled variant
 // For the common case of a CNHW activation (X is then a plain row-major [K][ncols] matrix with
 // leading dimension x_sC) with ncols % 4 == 0: both operands are staged through LDS with
@@ -244,7 +276,11 @@ void gemm_tiled_kernel(const GemmParams P, int mblocks, int nct, int vec) {
 // the A fragment X^T[n0 + lane % 32][k] stays L1/L2-resident (the 4 waves of a workgroup share
 // it: 32 images x 4 M-tiles).  The next 32-deep K-chunk's fragments are loaded while the
 // current chunk's 16 MFMAs run.
-template <bool FULLPLANE>
+// NCH > 0: the K loop fully unrolled for exactly NCH 32-deep chunks (the FaceMesh heads: K = 288,
+// 9 chunks).  The runtime loop's back edge makes the compiler's wait counting drain every load
+// (vmcnt(0)) before each chunk's MFMAs, prefetched chunk included; straight-line code keeps the
+// next chunk's loads in flight.  Same k order, same bits.
+template <bool FULLPLANE, int NCH>
 __global__ __launch_bounds__(256) void gemm_rows_kernel(const GemmParams P, int mtiles) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int kh = lane >> 5, col = lane & 31;
@@ -284,7 +320,15 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(const GemmParams P, int 
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     load(0, 0);
-    for (int kc = 0; kc < P.Kpad; kc += 2 * KC) {
+    if constexpr (NCH > 0) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            if (c + 1 < NCH) load((c + 1) * KC, (c + 1) & 1);
+#pragma unroll
+            for (int s = 0; s < KC / 2; ++s)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c & 1][s], b[c & 1][s], acc, 0, 0, 0);
+        }
+    } else for (int kc = 0; kc < P.Kpad; kc += 2 * KC) {
         if (kc + KC < P.Kpad) load(kc + KC, 1);
 #pragma unroll
         for (int s = 0; s < KC / 2; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][s], b[0][s], acc, 0, 0, 0);
@@ -373,10 +417,23 @@ const char *launch_gemm(const GemmParams &p, hipStream_t s) {
     }
     if (p.P == 1 && p.res_mode == 0 && p.KK > 1 && form_on(FORM_ROWS)) {  // a head over whole planes (KK >= 2)
         dim3 grid((p.ncols + 31) / 32, (mtiles + 3) / 4);
-        hipLaunchKernelGGL((gemm_rows_kernel<true>), grid, dim3(256), 0, s, p, mtiles);
-        return "gemm_rows_kernel<true>";
+        if ((p.Kpad + KC - 1) / KC == 9) {
+            hipLaunchKernelGGL((gemm_rows_kernel<true, 9>), grid, dim3(256), 0, s, p, mtiles);
+            return "gemm_rows_kernel<true, 9>";
+        }
+        hipLaunchKernelGGL((gemm_rows_kernel<true, 0>), grid, dim3(256), 0, s, p, mtiles);
+        return "gemm_rows_kernel<true, 0>";
     }
     const int bx = (p.ncols + 127) / 128;
+    const int nch = (p.Kpad + KC - 1) / KC;
+    if (p.KK == 1 && mtiles == 1 && nch <= 4 && form_on(FORM_ROWS)) {
+        switch (nch) {
+        case 1: hipLaunchKernelGGL((gemm_smallk_kernel<1>), dim3(bx), dim3(256), 0, s, p); return "gemm_smallk_kernel<1>";
+        case 2: hipLaunchKernelGGL((gemm_smallk_kernel<2>), dim3(bx), dim3(256), 0, s, p); return "gemm_smallk_kernel<2>";
+        case 3: hipLaunchKernelGGL((gemm_smallk_kernel<3>), dim3(bx), dim3(256), 0, s, p); return "gemm_smallk_kernel<3>";
+        default: hipLaunchKernelGGL((gemm_smallk_kernel<4>), dim3(bx), dim3(256), 0, s, p); return "gemm_smallk_kernel<4>";
+        }
+    }
     // Largest M tile (operand reuse) that still leaves >= 2 workgroups per CU of parallelism.
     int mt = 4;
     while (mt > 1 && (int64_t)bx * ((mtiles + mt - 1) / mt) < 512) --mt;
