@@ -801,7 +801,7 @@ const char *dwpw_go(const DwPwParams &p, hipStream_t s) {
     const int mb = (p.g.Mpad + BM - 1) / BM;
     dim3 grid((nct + 7) / 8 * 8, mb);
     int runmax = 0, bufsz = 0;
-    if constexpr ((K == 3 && MTW == 1) || K == 5) {
+    if constexpr (K == 3 && MTW == 1) {
         // wider channel chunks: fewer dependent DMA round trips per tile (the 6^2 / 3^2 launches
         // of a few dozen workgroups are nothing but those round trips)
         if (dfkc_max() >= 64)
