@@ -672,7 +672,7 @@ def hand_tracking_line(H, args, device, wl, streams=256, slots=4):
 RST_MCUS = 4  # restart interval of the JPEG-source frames (MCUs): 2040 intervals per 1080p 4:2:0 frame
 
 
-def jpeg_line(args, device, n_distinct=32, n_decodes=2048, threads=16, batch=8):
+def jpeg_line(args, device, n_distinct=32, n_decodes=2048, threads=16, batch=16):
     """1080p JPEG -> RGBA8 frames in HBM, byte-identical to the reference's
     libjpeg-turbo backend.  `threads` host threads (camera ingest workers) each own a decoder
     and a HIP stream (ctypes releases the GIL) and decode `batch` frames per call
