@@ -9,9 +9,12 @@ LandmarkTracker pass seeded from the best detection, examples/facemesh.rs:40-54 
 landmark.rs:463-501): GPU letterbox preprocessing + BlazeFace, exact host decode + weighted NMS,
 GPU ROI preprocessing + FaceMesh, host landmark mapping, loss check and ROI update.  Steps run
 back to back, software-pipelined (the next step's detections are enqueued before this step's
-landmark mapping).  With N > 1 every rank all-gathers each step's fixed-size detection records
-over RCCL (the single collective of SURVEY.md §8e) on the collective's own stream, overlapped
-with the following steps, inside the timed region.
+landmark mapping).  With N > 1 the post-processing kernel writes each step's fixed-size
+detection records straight into a device buffer and every rank all-gathers them over RCCL (the
+single collective of SURVEY.md §8e, zr_comm_all_gather_async) on the pipeline's own gather
+stream, overlapped with the following steps, inside the timed region: no host copy per step.
+torch.distributed (gloo) is the control plane only (the communicator id, barriers, the max of
+the per-rank times).
 
 `value` = tracked faces (face_flag >= the 0.5 loss threshold) per second over all ranks.
 
@@ -383,9 +386,10 @@ def prime(workloads, seconds, pool):
 
 
 def run_steps(workloads, steps, gather, rank, world, pool):
-    """`steps` software-pipelined steps of every workload (concurrently when there are two),
-    each step's detection records all-gathered asynchronously (world > 1)."""
-    from zaru_amd import shard
+    """`steps` software-pipelined steps of every workload (concurrently when there are two).  With
+    N > 1 each pipeline all-gathers its device-written records itself (RCCL, enable_records);
+    `gather` is only the shared-GPU dry run's stand-in (gloo has no device path: the records are
+    copied to the host and gathered there)."""
     for w in workloads:
         w.pipe.begin_steps()
     for k in range(steps):
@@ -396,9 +400,7 @@ def run_steps(workloads, steps, gather, rank, world, pool):
         else:
             list(pool.map(lambda w: w.pipe.step(more), workloads))
         if gather is not None:
-            # global frame ids: rank + world * i, the second workload's after the first's
-            recs = [w.pipe.detection_records(shard.REC_DETS, rank + j * world * w.batch, world)
-                    for j, w in enumerate(workloads)]
+            recs = [w.pipe.records() for w in workloads]
             gather.submit(np.concatenate(recs) if len(recs) > 1 else recs[0])
     if gather is not None:
         gather.finish()
@@ -439,10 +441,13 @@ def main():
     device = 0 if (share or world == 1) else local
     torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("gloo" if share else "nccl")
+        # one node: the RCCL bootstrap needs no network interface beyond loopback
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        dist.init_process_group("gloo")  # control plane only (ids, barriers, max / sum)
 
     import zaru_amd.host as H
     from zaru_amd import shard
+    from zaru_amd._lib import Comm
 
     kinds = ["face", "hand"] if args.workload == "both" else [primary]
     threads = args.threads if len(kinds) == 1 else max(2, args.threads // 2)
@@ -450,8 +455,24 @@ def main():
     for k in kinds:  # config 5: the hand pipeline runs on the face pipeline's frames
         wls.append(Workload(H, k, device, args.batch, rank, threads, args.sub_batches,
                             args.streams == "multi", shared=wls[0] if wls else None))
-    gather = (shard.RecordGather(args.batch * len(wls), shard.record_width(),
-                                 "cpu" if share else f"cuda:{device}") if world > 1 else None)
+    comms, gather = [], None
+    if world > 1:
+        if not share:
+            # the data-path communicators: RCCL over xGMI, one rank per GPU; one per pipeline, since
+            # config 5's two pipelines step from two host threads and a communicator's collectives
+            # must be issued in the same order on every rank
+            for _ in wls:
+                uid = torch.zeros(128, dtype=torch.uint8)
+                if rank == 0:
+                    uid.copy_(torch.frombuffer(bytearray(Comm.unique_id()), dtype=torch.uint8))
+                dist.broadcast(uid, 0)
+                comms.append(Comm(bytes(uid.numpy().tobytes()), world, rank, device))
+        else:
+            gather = shard.RecordGather(args.batch * len(wls), shard.record_width(), "cpu")
+        # global frame ids: rank + world * i, the second workload's after the first's
+        for j, w in enumerate(wls):
+            w.pipe.enable_records(shard.REC_DETS, rank + j * world * w.batch, world,
+                                  comms[j].ptr if comms else 0, world)
     pool = None
     if len(wls) > 1:
         from concurrent.futures import ThreadPoolExecutor
@@ -470,16 +491,23 @@ def main():
     elapsed = time.perf_counter() - t0
 
     counts = np.array([[t["tracked"], t["rois"], t["frames"], t["detections"]] for t in times], np.float64)
+    gather_check = None
+    if comms:  # the last step's gathered records: every rank's frames, ids as assigned
+        g = wls[0].pipe.gathered()
+        ids = np.sort(g[:, 0].view(np.uint32))
+        gather_check = bool(np.array_equal(ids, np.arange(world * args.batch, dtype=np.uint32)))
     if world > 1:
-        red_dev = "cpu" if share else f"cuda:{device}"
-        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
+        t = torch.tensor([elapsed], dtype=torch.float64)  # gloo control group: host tensors
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        c = torch.from_numpy(counts).to(red_dev)
+        c = torch.from_numpy(counts)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        counts = c.cpu().numpy()
+        counts = c.numpy()
     if rank != 0:
         if world > 1:
+            torch.cuda.synchronize()
+            for c in comms:
+                c.close()
             dist.destroy_process_group()
         return
 
@@ -487,6 +515,9 @@ def main():
     tracked, rois, frames, dets = counts[0]
     stage = {k: round(times[0][k] / args.steps, 3)
              for k in ("detect_gpu_ms", "decode_nms_ms", "landmark_gpu_ms", "map_ms")}
+    if Workload.device_post:  # device mode: the stages are kernels (names as the reference's timers)
+        stage = {"infer_detector_ms": stage["detect_gpu_ms"], "extract_nms_map_seed_ms": stage["decode_nms_ms"],
+                 "infer_landmarks_ms": stage["landmark_gpu_ms"], "track_update_ms": stage["map_ms"]}
     frames_per_s_gpu = frames / elapsed / world
     # SURVEY §8d pipeline model: detector + (landmark net per ROI) + both preprocessings
     din, lin = WORKLOADS[wl.kind][2], WORKLOADS[wl.kind][3]
@@ -519,14 +550,21 @@ def main():
                    "frames_per_gpu_per_step": args.batch, "frame": "1920x1080 RGBA8",
                    "sub_batches": args.sub_batches, "streams": args.streams,
                    "parallelism": f"frame-sharded x{world}"
-                   + ((", one async gloo all-gather of detection records per step (shared-GPU dry run)" if share
-                       else ", one async RCCL all-gather of detection records per step") if world > 1 else "")},
+                   + ((", device-written detection records copied to the host and all-gathered over gloo "
+                       "each step (shared-GPU dry run: gloo has no device path)" if share
+                       else ", one RCCL all-gather per step of the detection records the post-processing "
+                       "kernel writes on the device, on the pipeline's gather stream") if world > 1 else "")},
         "prime": primed,
+        "gather_check": gather_check,
         "frames_per_s": round(frames / elapsed, 1),
         "rois_per_s": round(rois / elapsed, 1),
         "tracked_per_step": round(tracked / args.steps / world, 2),
         "detections_per_step": round(dets / args.steps / world, 2),
         "stage_ms_per_step": stage,
+        "stage_timing": ("HIP-event spans of each stage on the sub-batch streams, summed over the "
+                         "concurrent sub-batches (detector / decode+NMS+map+ROI seeding / landmark "
+                         "network / tracker update)") if Workload.device_post else "host waits and host work",
+        "host_wait_ms_per_step": round(times[0]["host_wait_ms"] / args.steps, 3),
         "pipeline_roofline": {
             "model": "SURVEY.md §8d: fixed algorithmic bytes per frame (detector + preprocessing + "
                      "landmark net per ROI), fp32 activations at layer boundaries",
@@ -562,6 +600,9 @@ def main():
     out["cpu_baseline"] = cpu
     print(json.dumps(out))
     if world > 1:
+        torch.cuda.synchronize()
+        for c in comms:
+            c.close()
         dist.destroy_process_group()
 
 

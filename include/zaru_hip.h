@@ -105,24 +105,38 @@ int zr_detection_candidates_async(const float *d_logits, const float *d_boxes, u
                                   uint32_t cap, int32_t *d_count, float *d_rec, void *hip_stream);
 
 /* ---- Detector::detect_impl after inference, on the device ----------------------------------
- * extract_outputs + weighted NMS (Average) + map into frame pixels (crates/zaru/src/
- * detection.rs:231-267, face/detection.rs:96-157, hand/detection.rs:108-179, detection/nms.rs:
- * 59-145), one wave per frame, bit-exact with the host restatement (glibc expf / atan2f restated
- * on the device; NMS ties in anchor order).  Per frame: d_count[f] = detections after NMS, the
+ * extract_outputs + NMS + map into frame pixels (crates/zaru/src/detection.rs:231-267,
+ * face/detection.rs:96-157, hand/detection.rs:108-179, detection/nms.rs:59-145), one wave per
+ * frame, bit-exact with the host restatement (glibc expf / atan2f restated on the device; NMS ties
+ * in anchor order).  Per frame: d_count[f] = detections after NMS (exact, whatever dcap is), the
  * first dcap of them in d_dets [n][dcap][20] = {conf, angle, cx, cy, w, h, 7 x (kx, ky)} (frame
- * px, keypoints past the network's zero), and when d_records is not NULL the all-gather record
- * [n][2 + 20 rmax] = {frame id first_id + f * id_stride (u32 bits), count (u32 bits), the first
- * rmax detections}. */
+ * px, keypoints past the network's zero; dcap = anchors keeps every detection), and when d_records
+ * is not NULL the all-gather record [n][2 + 20 rmax] = {frame id first_id + f * id_stride (u32
+ * bits), count (u32 bits), the first rmax detections, zeros}. */
 typedef struct {
     int face;               /* 1 BlazeFace (angle: eye line vs +X), 0 BlazePalm (wrist -> MCP vs +Y) */
     int anchors, params, keypoints;  /* A, values per anchor (16 / 18), keypoints (6 / 7) */
     int in_w, in_h;         /* detector input */
     float thresh, iou;      /* Detector threshold (0.5), NMS IoU threshold (0.3) */
+    int mode;               /* SuppressionMode (nms.rs:154-163): 0 Average (default), 1 Remove */
 } zr_detpost_cfg;
 int zr_detect_post_async(const float *d_logits, const float *d_boxes, const float *d_anchors,
                          const float *d_letterbox, size_t n, const zr_detpost_cfg *cfg,
                          int32_t *d_count, float *d_dets, size_t dcap, float *d_records, size_t rmax,
                          uint32_t first_id, uint32_t id_stride, void *hip_stream);
+
+/* ---- the one collective of the multi-GPU path ------------------------------
+ * A communicator over the node's ranks (one process per GPU) for the all-gather of the detection
+ * records (RCCL over xGMI).  The reference has no multi-device code; this is the build's own
+ * exchange, issued on a HIP stream so it overlaps the next step's kernels.  zr_comm_unique_id
+ * runs on one rank; its 128 bytes reach the others by any side channel (the benchmark uses the
+ * gloo control group).  zr_comm_create blocks until every rank joined. */
+typedef struct zr_comm zr_comm;
+int zr_comm_unique_id(uint8_t id[128]);
+int zr_comm_create(const uint8_t id[128], int nranks, int rank, int device, zr_comm **out);
+void zr_comm_destroy(zr_comm *c);
+/* recv (nranks * bytes, rank-major) <- every rank's send (bytes), enqueued on hip_stream */
+int zr_comm_all_gather_async(zr_comm *c, const void *d_send, void *d_recv, size_t bytes, void *hip_stream);
 
 /* ---- LandmarkTracker state on the device ------------------------------
  * A video loop of LandmarkTracker::track (crates/zaru/src/landmark.rs:463-501) over n streams
@@ -196,8 +210,9 @@ int zr_track_seed_detections_async(const int32_t *d_count, const float *d_dets, 
  * consumed the previous step's hand landmark estimate: drops lost hands (tracking.rs:116-127);
  * when d_det_pending[s], filters stream s's palm detections (d_count / d_dets as
  * zr_detect_post_async writes them, frame px) against the hands' ROIs (136-156) and starts a hand
- * for each kept one, ROI = RotatedRect(det.rect.grow_rel(palm_grow), det.angle) (158-194, ids from
- * d_next_id; past H slots a detection is dropped); removes hands whose ROI overlaps an earlier
+ * for each kept one, ROI = RotatedRect(det.rect.grow_rel(palm_grow), det.angle) (158-194, u64 HandIds
+ * from d_next_id; a kept detection finding no free slot of the H is counted in d_dropped[s], may be
+ * NULL -- the reference's Vec grows instead); removes hands whose ROI overlaps an earlier
  * hand's with the reference's swap_remove sweep (196-208); and sets d_det_pending[s] when no hand
  * is left or now_ms reached d_next_det[s] (advanced by interval_ms) -- this step's palm detection
  * then counts at the next call (210-218).  Writes every slot's view (idle slots: an empty view),
@@ -211,11 +226,11 @@ typedef struct {
     double interval_ms;     /* redetection interval, tracking.rs:41 (300 ms) */
     int aspect_w, aspect_h; /* the hand landmark network's aspect ratio */
 } zr_hand_cfg;
-int zr_hand_manage_async(zr_track_state *d_state, uint32_t *d_ids, float *d_hroi, int32_t *d_src,
-                         int32_t *d_nhands, uint32_t *d_next_id, double *d_next_det, int32_t *d_det_pending,
+int zr_hand_manage_async(zr_track_state *d_state, uint64_t *d_ids, float *d_hroi, int32_t *d_src,
+                         int32_t *d_nhands, uint64_t *d_next_id, double *d_next_det, int32_t *d_det_pending,
                          const int32_t *d_count, const float *d_dets, size_t dcap,
                          const uint32_t *d_frame_size, size_t n, const zr_hand_cfg *cfg, double now_ms,
-                         int init_clock, zr_view_desc *d_views, void *hip_stream);
+                         int init_clock, zr_view_desc *d_views, int32_t *d_dropped, void *hip_stream);
 /* Cnn::estimate (nn/mod.rs:118-126) with a device-resident view table (frames: host array). */
 int zr_cnn_estimate_device_views_async(zr_session *s, const zr_frame *frames, size_t n_frames,
                                        const zr_view_desc *d_views, size_t n_views, float lo,
@@ -250,10 +265,15 @@ typedef struct {
     uint32_t bw[3], bh[3], qsel[3];
     uint16_t quant[4][64]; /* natural order */
 } zr_jpeg_layout;
-/* Frames decoded so far whose Huffman stage ran on the device (streams with restart intervals:
- * one lane per interval) and on the host; *corrupt (may be NULL; waits for the last decode) is 1
- * when a device-decoded stream held an invalid Huffman code or AC index since creation. */
+/* Frames decoded so far whose Huffman stage ran on the device and on the host; *corrupt (may be
+ * NULL; waits for the last call) is 1 when a frame of the LAST call held an invalid Huffman code or
+ * AC index.  Error contract: a frame decoded on the host with corrupt data fails the call
+ * (ZR_ERR_INVALID_ARGUMENT, frame named); on the device it cannot fail the already-returned call,
+ * so the rest of the corrupt interval decodes as all-zero blocks (libjpeg-turbo's insufficient-
+ * data behaviour) and the frame's flag is set -- zr_jpeg_frame_errors names the frames. */
 int zr_jpeg_decoder_status(zr_jpeg_decoder *d, uint64_t *gpu_entropy, uint64_t *host_entropy, int *corrupt);
+/* per frame of the last call: 1 = corrupt entropy data (waits for that call); *n = its frame count */
+int zr_jpeg_frame_errors(zr_jpeg_decoder *d, int32_t *flags, size_t cap, size_t *n);
 int zr_jpeg_coefficients(const uint8_t *jpeg, size_t len, int16_t *coef, size_t cap_blocks,
                          zr_jpeg_layout *layout);
 
@@ -289,10 +309,16 @@ int zr_free(void *p);
 int zr_host_alloc(void **p, size_t bytes); /* page-locked host memory (truly async copies) */
 int zr_host_free(void *p);
 int zr_memcpy_async(void *dst, const void *src, size_t bytes, int kind, void *hip_stream);
+/* height rows of width bytes, row pitches dpitch / spitch */
+int zr_memcpy2d_async(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t height,
+                      int kind, void *hip_stream);
 int zr_stream_create(void **stream);
 int zr_stream_destroy(void *stream);
 int zr_stream_synchronize(void *stream);
 int zr_event_create(void **event);
+int zr_event_create_timing(void **event); /* an event zr_event_elapsed can read */
+int zr_event_elapsed(float *ms, void *start, void *end);
+int zr_stream_wait_event(void *stream, void *event);
 int zr_event_destroy(void *event);
 int zr_event_record(void *event, void *stream);
 int zr_event_synchronize(void *event);

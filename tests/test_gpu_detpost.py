@@ -19,7 +19,8 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 class Cfg(C.Structure):
     _fields_ = [("face", C.c_int), ("anchors", C.c_int), ("params", C.c_int), ("keypoints", C.c_int),
-                ("in_w", C.c_int), ("in_h", C.c_int), ("thresh", C.c_float), ("iou", C.c_float)]
+                ("in_w", C.c_int), ("in_h", C.c_int), ("thresh", C.c_float), ("iou", C.c_float),
+                ("mode", C.c_int)]
 
 
 @pytest.mark.parametrize("net", ["face", "palm"])

@@ -83,19 +83,72 @@ def test_device_hand_tracker_matches_host(H):
     assert checked >= 10, checked
 
 
+def _many_hands(H):
+    """six palm detections far apart (all kept) plus one on top of the first (filtered on the next
+    detection pass only when tracked -- here both arrive together, so the sweep removes it)"""
+    R = H.Rect.from_center
+    dets = [H.Detection(0.9, R(50.0 + 75.0 * i, 60.0 + 40.0 * (i % 2), 16.0, 16.0), 0.1 * i) for i in range(6)]
+    dets.append(H.Detection(0.8, R(52.0, 61.0, 16.0, 16.0), 0.0))
+    return dets
+
+
+@pytest.mark.parametrize("slots", [8, 3])
+def test_device_hand_tracker_capacity_against_host(H, slots):
+    """More kept palm detections than a small slot count: the device keeps the first `slots` hands
+    exactly as the host HandTracker orders them and reports the rest as dropped (the reference's
+    hand list grows instead, tracking.rs:158-194); with enough slots it equals the host outright."""
+    from zaru_amd._lib import DeviceBuffer
+    f = _frames(3, 21)
+    host = H.HandTracker()
+    host.set_loss_threshold(-1.0)
+    dev = H.DeviceHandTracker(1, slots)
+    dev.set_loss_threshold(-1.0)
+    host.inject_detections(_many_hands(H))
+    dev.inject_detections(0, _many_hands(H))
+    bufs = [DeviceBuffer.from_array(f[k]) for k in range(3)]
+    # with enough slots the two agree on every step; with fewer, on the step that started the
+    # hands (later de-duplication sweeps may swap_remove a host hand past the device's slots into
+    # an earlier position, which the capped device list cannot mirror)
+    steps = 3 if slots >= 7 else 1
+    dropped = []
+    for k in range(steps):
+        host.wait_detection()
+        host.track(f[k], now_ms=10.0 * k)
+        dev.step([(bufs[k].ptr, 480, 360, 480 * 4)], 10.0 * k)
+        dev.synchronize()
+        dropped.append(dev.dropped_hands()[0])
+        n_host = host.num_tracked()
+        assert dev.hand_counts()[0] == min(n_host, slots), (k, n_host)
+        want = host.hands()[:slots]
+        got = dev.hands(0)
+        assert [h["id"] for h in got] == [h["id"] for h in want], k
+        for g, w in zip(got, want):
+            assert g["view_rect"].rect() == w["view_rect"].rect(), (k, g["id"])
+            assert np.array_equal(g["landmarks"], w["landmarks"]), (k, g["id"])
+    # the step that consumed the seven detections: all 7 pass the filter (no hand yet); the sweep
+    # runs after the slots are filled, so 7 - slots found no slot when slots < 7
+    assert dropped[0] == max(0, 7 - slots), dropped
+    assert host.num_tracked() == 6 or steps > 1  # the sweep removed the overlapping seventh
+    assert dev.dropped_detections() == [0]
+    assert dev.detection_capacity() == 2016
+
+
 def test_device_hand_tracker_capacity_and_rejects(H):
-    # more kept detections than slots: the extra ones are dropped, ids stay dense
+    # more kept detections than slots: the extra ones are counted as dropped, ids stay dense
     from zaru_amd._lib import DeviceBuffer
     dev = H.DeviceHandTracker(1, 2)
     dev.set_loss_threshold(-1.0)
     f = _frames(2, 3)
     dets = [H.Detection(0.9, H.Rect.from_center(60.0 + 120.0 * i, 100.0, 30.0, 30.0), 0.0) for i in range(3)]
     dev.inject_detections(0, dets)
+    drops = []
     for k in range(2):
         b = DeviceBuffer.from_array(f[k])
         dev.step([(b.ptr, 480, 360, 480 * 4)], 10.0 * k)
         dev.synchronize()
+        drops.append(dev.dropped_hands()[0])
     assert dev.hand_counts() == [2]
     assert [h["id"] for h in dev.hands(0)] == [0, 1]
+    assert drops[0] == 1
     with pytest.raises(Exception):
         dev.step([], 0.0)

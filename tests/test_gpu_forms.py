@@ -30,7 +30,7 @@ for model, s in (("face_detection_short_range", 128), ("face_landmark", 192),
 np.savez(sys.argv[2], **out)
 """
 
-# each setting turns one form off ("-form") or the opt-in chain form on; "all_off" every form
+# each setting turns one form off ("-form"); "all_off" every form
 SWITCHES = {
     "default": "",
     "no_valu_db": "-valu_db",
@@ -40,9 +40,6 @@ SWITCHES = {
     "no_rows": "-rows",
     "no_vres": "-vres",
     "no_vstore": "-vstore",
-    "ir": "+ir",  # expand + depthwise + project as one launch (ir.hip), opt-in
-    "ring": "+ring",  # persistent LDS-ring MFMA dwpw (dwpw_mfma.hip), opt-in
-    "chain": "+chain",  # low-resolution layer runs in one launch per image (chain.hip)
     "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore",
 }
 
@@ -98,31 +95,3 @@ def test_nonsquare_full_plane_conv(forms):
     r = subprocess.run([sys.executable, "-c", NONSQUARE_CHILD, REPO], env=e, capture_output=True, text=True,
                        timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
-
-
-# A fused launch must not write over a tensor it still reads: the inverted-residual form (ir.hip)
-# reads the expand's input and writes the projection in one launch, so the arena must keep them
-# apart -- visible only at batches where later images' workgroups run after earlier ones wrote.
-LARGE_CHILD = r"""
-import sys, numpy as np
-sys.path.insert(0, sys.argv[1])
-from zaru_amd.nn import NeuralNetwork, model_bytes
-net = NeuralNetwork.from_onnx(model_bytes("hand_landmark_lite")).load()
-x = np.random.default_rng(9).uniform(-1.0, 1.0, size=(520, 3, 224, 224)).astype(np.float32)
-np.savez(sys.argv[2], *net.estimate(x))
-"""
-
-
-def test_fused_inverted_residual_large_batch(tmp_path):
-    # unfused (default), the 112^2 block fused (+ir), every eligible block fused (+ir, ZARU_HIP_IR_ALL)
-    res = {}
-    for name, env in (("default", {}), ("ir", {"ZARU_HIP_FORMS": "+ir"}),
-                      ("all", {"ZARU_HIP_FORMS": "+ir", "ZARU_HIP_IR_ALL": "1"})):
-        path = str(tmp_path / f"l_{name}.npz")
-        subprocess.run([sys.executable, "-c", LARGE_CHILD, REPO, path], check=True, timeout=110,
-                       env=dict(os.environ, **env))
-        with np.load(path) as z:
-            res[name] = [z[k] for k in z.files]
-    for other in ("ir", "all"):
-        for a, b in zip(res["default"], res[other]):
-            assert np.array_equal(a, b), (other, float(np.abs(a - b).max()))

@@ -232,9 +232,52 @@ def test_restart_stream_corrupt_interval_is_flagged(dec):
         out = d.decode(bytes(bad))
         assert out.shape == (480, 640, 4)
         assert d.status()[2] == 1
+        assert list(d.frame_errors()) == [True]
         assert np.array_equal(d.decode(data), libjpeg_turbo_rgba(data))
+        assert d.status()[2] == 0  # the flag is per call: the good frame after it is clean
     finally:
         d.close()
+
+
+def _corrupt_third_interval(data):
+    k = _scan_start(data)
+    bad = bytearray(data)
+    r = [i for i in range(k, len(data) - 1) if data[i] == 0xFF and 0xD0 <= data[i + 1] <= 0xD7]
+    p = (r[1] + r[2]) // 2
+    while data[p - 1] == 0xFF:
+        p += 1
+    bad[p:p + 16] = b"\xff\x00" * 8
+    return bytes(bad)
+
+
+def test_corrupt_interval_leaves_no_stale_coefficients(dec):
+    """After a corrupt symbol the rest of the interval decodes as all-zero blocks (libjpeg-turbo's
+    insufficient-data rule), never as whatever an earlier frame left in the reused coefficient
+    buffer: the corrupt frame decodes the same on a decoder that just decoded another camera's
+    frame as on a fresh one.  In a batch, only the corrupt frame is flagged."""
+    from zaru_amd._lib import DeviceBuffer, lib
+    from zaru_amd.jpeg import JpegDecoder
+    other = encode(synthetic(480, 640, 31), quality=90, restart_marker_blocks=2)
+    data = encode(synthetic(480, 640, 8), quality=90, restart_marker_blocks=2)
+    bad = _corrupt_third_interval(data)
+    fresh = JpegDecoder(0)
+    used = JpegDecoder(0)
+    try:
+        want = fresh.decode(bad)
+        used.decode(other)
+        got = used.decode(bad)
+        assert np.array_equal(got, want)
+        # the corruption really zeroed something: not the clean decode
+        assert not np.array_equal(want, libjpeg_turbo_rgba(data))
+        bufs = [DeviceBuffer(480 * 640 * 4) for _ in range(3)]
+        used.decode_batch_into([data, bad, other], [b.ptr for b in bufs], [640 * 4] * 3)
+        lib().zr_stream_synchronize(None)
+        assert list(used.frame_errors()) == [False, True, False]
+        assert np.array_equal(bufs[1].download((480, 640, 4), "uint8"), want)
+        assert np.array_equal(bufs[2].download((480, 640, 4), "uint8"), libjpeg_turbo_rgba(other))
+    finally:
+        fresh.close()
+        used.close()
 
 
 def test_restart_stream_cut_mid_scan(dec):

@@ -1,0 +1,33 @@
+#!/bin/bash
+# One GPU-box session through gpurun: usage  bash tools/gpu_run.sh <tag> <step>[,<step>...] [bench args]
+# steps: tests (pytest -m gpu), smoke, bench (default bench line), quick (face line only, no side
+# lines), both (config 5), n2 (shared-GPU N = 2 dry run via torchrun, gloo gather), prof
+# (rocprofv3 --kernel-trace --stats of the face line).  Each step has its own time limit; the
+# chain stops at the first failure.
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+TAG=${1:-r04}; STEPS=${2:-tests,smoke}; shift 2
+O=gpurun_out/$TAG && mkdir -p $O || exit 1
+NOSIDE="--no-hand --no-next --no-tracking --no-jpeg --no-c5"
+for s in ${STEPS//,/ }; do
+  case $s in
+    tests) timeout -k 10 500 python -u -m pytest tests -m gpu -v -rP --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 ;;
+    smoke) timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 ;;
+    bench) timeout -k 10 700 python bench.py "$@" > $O/bench.json 2> $O/bench.err ;;
+    quick) timeout -k 10 300 python bench.py --no-cpu-baseline --no-traffic $NOSIDE "$@" > $O/quick.json 2> $O/quick.err ;;
+    hand) timeout -k 10 300 python bench.py --workload hand --batch 256 --steps 30 --warmup 5 --no-cpu-baseline --no-traffic "$@" > $O/hand.json 2> $O/hand.err ;;
+    both) timeout -k 10 300 python bench.py --workload both --steps 30 --warmup 5 --no-cpu-baseline --no-traffic --no-profile "$@" > $O/both.json 2> $O/both.err ;;
+    n1) timeout -k 10 300 python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-traffic --no-profile $NOSIDE "$@" > $O/n1.json 2> $O/n1.err ;;
+    n2) ZARU_BENCH_SHARE_GPU=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+          --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 50 --warmup 10 --no-cpu-baseline \
+          --no-traffic --no-profile $NOSIDE "$@" > $O/n2.json 2> $O/n2.err ;;
+    n2half) ZARU_BENCH_SHARE_GPU=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+          --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 2 --batch 512 --steps 50 --warmup 10 \
+          --no-cpu-baseline --no-traffic --no-profile $NOSIDE "$@" > $O/n2half.json 2> $O/n2half.err ;;
+    prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py \
+          --steps 20 --warmup 5 --no-cpu-baseline --no-traffic $NOSIDE "$@" > $O/bench_prof.json 2> $O/prof.err ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+  rc=$?
+  echo "$s rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+done

@@ -56,7 +56,11 @@ SIGNATURES = [
     ("zr_detect_post_async", _I, [_P, _P, _P, _P, _SZ, _P, _P, _P, _SZ, _P, _SZ, _U32, _U32, _P]),
     ("zr_track_seed_detections_async", _I, [_P, _P, _SZ, _P, _P, _P, _SZ, _P, _F, _I, _P, _P, _P, _P]),
     ("zr_hand_manage_async", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P, _SZ, _P, C.c_double, _I,
-                                  _P, _P]),
+                                  _P, _P, _P]),
+    ("zr_comm_unique_id", _I, [_P]),
+    ("zr_comm_create", _I, [_P, _I, _I, _I, C.POINTER(_P)]),
+    ("zr_comm_destroy", None, [_P]),
+    ("zr_comm_all_gather_async", _I, [_P, _P, _P, _SZ, _P]),
     ("zr_debug_glibc_math", _I, [_I, _P, _P, _P, _SZ, _P]),
     ("zr_cnn_estimate_device_views_async", _I, [_P, _P, _SZ, _P, _SZ, _F, _F, _P, _P]),
     ("zr_jpeg_decoder_create", _I, [C.c_int, _P]),
@@ -66,6 +70,7 @@ SIGNATURES = [
     ("zr_jpeg_decode_batch_async", _I, [_P, _SZ, _P, _P, _P, _P, _P]),
     ("zr_jpeg_coefficients", _I, [_P, _SZ, _P, _SZ, _P]),
     ("zr_jpeg_decoder_status", _I, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(_I)]),
+    ("zr_jpeg_frame_errors", _I, [_P, _P, _SZ, C.POINTER(_SZ)]),
     ("zr_session_stats", _I, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(_SZ)]),
     ("zr_plan_describe", _I, [_P, _SZ, _P, _SZ, _P, _SZ, C.POINTER(_SZ)]),
     ("zr_profile_enable", _I, [_P, _I]),
@@ -77,10 +82,14 @@ SIGNATURES = [
     ("zr_host_alloc", _I, [C.POINTER(_P), _SZ]),
     ("zr_host_free", _I, [_P]),
     ("zr_memcpy_async", _I, [_P, _P, _SZ, _I, _P]),
+    ("zr_memcpy2d_async", _I, [_P, _SZ, _P, _SZ, _SZ, _SZ, _I, _P]),
     ("zr_stream_create", _I, [C.POINTER(_P)]),
     ("zr_stream_destroy", _I, [_P]),
     ("zr_stream_synchronize", _I, [_P]),
     ("zr_event_create", _I, [C.POINTER(_P)]),
+    ("zr_event_create_timing", _I, [C.POINTER(_P)]),
+    ("zr_event_elapsed", _I, [C.POINTER(_F), _P, _P]),
+    ("zr_stream_wait_event", _I, [_P, _P]),
     ("zr_event_destroy", _I, [_P]),
     ("zr_event_record", _I, [_P, _P]),
     ("zr_event_synchronize", _I, [_P]),
@@ -167,3 +176,34 @@ class DeviceBuffer:
 
 def synchronize(stream=None):
     check(lib().zr_stream_synchronize(stream))
+
+
+class Comm:
+    """The node communicator of the multi-GPU path (zr_comm_*): RCCL over xGMI,
+    one rank per GPU.  `unique_id()` on one rank; its 128 bytes reach the others by any side
+    channel (bench.py: the gloo control group); `Comm(uid, world, rank, device)` joins."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * 128)()
+        check(lib().zr_comm_unique_id(buf))
+        return bytes(buf)
+
+    def __init__(self, uid: bytes, world: int, rank: int, device: int):
+        if len(uid) != 128:
+            raise ValueError("a communicator id is 128 bytes")
+        p = C.c_void_p()
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        check(lib().zr_comm_create(buf, world, rank, device, C.byref(p)))
+        self.ptr, self.world, self.rank = p.value, world, rank
+
+    def all_gather_async(self, d_send: int, d_recv: int, nbytes: int, stream=None):
+        check(lib().zr_comm_all_gather_async(self.ptr, d_send, d_recv, nbytes, stream))
+
+    def close(self):
+        if getattr(self, "ptr", None) and _LIB is not None:
+            _LIB.zr_comm_destroy(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        self.close()

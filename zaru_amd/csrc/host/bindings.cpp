@@ -312,6 +312,9 @@ PYBIND11_MODULE(_zaru_host, m) {
         .def("synchronize", &DeviceHandTracker::synchronize, py::call_guard<py::gil_scoped_release>())
         .def("hand_counts", &DeviceHandTracker::hand_counts)
         .def("detection_pending", &DeviceHandTracker::detection_pending)
+        .def("dropped_hands", &DeviceHandTracker::dropped_hands)
+        .def("dropped_detections", &DeviceHandTracker::dropped_detections)
+        .def("detection_capacity", &DeviceHandTracker::detection_capacity)
         .def("hands", [](DeviceHandTracker &t, size_t s) {
             py::list out;
             for (auto &h : t.hands(s)) {
@@ -392,7 +395,8 @@ PYBIND11_MODULE(_zaru_host, m) {
     py::class_<DetectTrackPipeline>(m, "DetectTrackPipeline")
         .def(py::init([](const std::string &kind, int device, int threads, uint32_t max_rois,
                          uint32_t sub_batches, bool stream_per_sub_batch, float loss_threshold,
-                         const std::string &detector, const std::string &landmarker, bool device_post) {
+                         const std::string &detector, const std::string &landmarker, bool device_post,
+                         const std::string &nms_mode, uint32_t det_cap, float det_threshold) {
                  PipelineConfig c = kind == "hand" ? PipelineConfig::hand() : PipelineConfig::face();
                  if (kind != "hand" && kind != "face")
                      throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "pipeline kind must be 'face' or 'hand'");
@@ -405,12 +409,18 @@ PYBIND11_MODULE(_zaru_host, m) {
                  c.stream_per_sub_batch = stream_per_sub_batch;
                  c.loss_threshold = loss_threshold;  // LandmarkTracker::set_loss_threshold
                  c.device_post = device_post;
+                 if (nms_mode == "remove") c.nms_mode = SuppressionMode::Remove;  // Detector::nms_mut
+                 else if (nms_mode != "average") throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "nms_mode: average | remove");
+                 c.det_cap = det_cap;
+                 c.det_threshold = det_threshold;  // Detector::set_threshold (detection.rs:191-193)
                  return new DetectTrackPipeline(c, device, threads);
              }), py::arg("kind") = "face", py::arg("device") = 0, py::arg("threads") = 8,
              py::arg("max_rois_per_frame") = 8, py::arg("sub_batches") = 2,
              py::arg("stream_per_sub_batch") = true,
              py::arg("loss_threshold") = LandmarkTracker::DEFAULT_LOSS_THRESHOLD,
-             py::arg("detector") = "", py::arg("landmarker") = "", py::arg("device_post") = true)
+             py::arg("detector") = "", py::arg("landmarker") = "", py::arg("device_post") = true,
+             py::arg("nms_mode") = "average", py::arg("det_cap") = 0,
+             py::arg("det_threshold") = Detector::DEFAULT_THRESHOLD)
         // frames: list of (device ptr, width, height, row_stride); forced: per frame list of
         // (cx, cy, w, h, rad) ROIs used when the frame has no detection
         .def("run", [](DetectTrackPipeline &p, const std::vector<std::tuple<uint64_t, uint32_t, uint32_t, uint64_t>> &frames,
@@ -479,6 +489,35 @@ PYBIND11_MODULE(_zaru_host, m) {
             pack_detection_records(d, ids, rmax, a.mutable_data());
             return a;
         }, py::arg("rmax") = 8, py::arg("first_id") = 0, py::arg("id_stride") = 1)
+        // device-written records, all-gathered over `comm` (a zaru_amd._lib.Comm
+        // pointer, 0: none) on the pipeline's own stream
+        .def("enable_records", [](DetectTrackPipeline &p, uint32_t rmax, uint32_t first_id, uint32_t id_stride,
+                                  uint64_t comm, int world) {
+            p.enable_records(rmax, first_id, id_stride, reinterpret_cast<zr_comm *>(comm), world);
+        }, py::arg("rmax") = 8, py::arg("first_id") = 0, py::arg("id_stride") = 1, py::arg("comm") = 0,
+           py::arg("world") = 1)
+        .def("records", [](DetectTrackPipeline &p) {
+            std::vector<float> r;
+            {
+                py::gil_scoped_release nogil;
+                r = p.records();
+            }
+            const py::ssize_t w = p.record_width();
+            py::array_t<float> a({(py::ssize_t)r.size() / w, w});
+            std::memcpy(a.mutable_data(), r.data(), r.size() * 4);
+            return a;
+        })
+        .def("gathered", [](DetectTrackPipeline &p) {
+            std::vector<float> r;
+            {
+                py::gil_scoped_release nogil;
+                r = p.gathered();
+            }
+            const py::ssize_t w = p.record_width();
+            py::array_t<float> a({(py::ssize_t)r.size() / w, w});
+            std::memcpy(a.mutable_data(), r.data(), r.size() * 4);
+            return a;
+        })
         .def("num_rois", [](const DetectTrackPipeline &p) { return p.rois().size(); })
         .def("roi", [](const DetectTrackPipeline &p, size_t i) {
             const RoiResult &r = p.rois().at(i);
@@ -501,6 +540,8 @@ PYBIND11_MODULE(_zaru_host, m) {
             d["landmark_gpu_ms"] = t.landmark_gpu_ms;
             d["map_ms"] = t.map_ms;
             d["total_ms"] = t.total_ms;
+            d["host_wait_ms"] = t.host_wait_ms;
+            d["dropped_detections"] = t.dropped_detections;
             d["frames"] = t.frames;
             d["detections"] = t.detections;
             d["rois"] = t.rois;

@@ -37,6 +37,7 @@ DeviceHandTracker::DeviceHandTracker(size_t streams, int slots, int device)
     pcfg_.in_h = (int)palm_->input_height();
     pcfg_.thresh = Detector::DEFAULT_THRESHOLD;
     pcfg_.iou = NonMaxSuppression::DEFAULT_IOU_THRESH;
+    dcap_ = palm_net_.anchors().size();
     check(zr_stream_create(&stream_));
     const size_t nv = n_ * (size_t)slots;
     state_.resize(nv);
@@ -50,6 +51,7 @@ DeviceHandTracker::DeviceHandTracker(size_t streams, int slots, int device)
     next_det_.resize(n_);
     det_pending_.resize(n_);
     count_.resize(n_);
+    dropped_.resize(n_);
     fsize_.resize(2 * n_);
     lbox_.resize(4 * n_);
     dets_.resize(n_ * dcap_ * 20);
@@ -64,10 +66,12 @@ DeviceHandTracker::DeviceHandTracker(size_t streams, int slots, int device)
     const std::vector<zr_track_state> zs(nv, zr_track_state{});
     check(zr_memcpy_async(state_.ptr, zs.data(), nv * sizeof(zr_track_state), 0, stream_));
     const std::vector<int32_t> zi(n_, 0);
+    const std::vector<uint64_t> zl(n_, 0);
     check(zr_memcpy_async(nhands_.ptr, zi.data(), n_ * 4, 0, stream_));
-    check(zr_memcpy_async(next_id_.ptr, zi.data(), n_ * 4, 0, stream_));
+    check(zr_memcpy_async(next_id_.ptr, zl.data(), n_ * 8, 0, stream_));
     check(zr_memcpy_async(det_pending_.ptr, zi.data(), n_ * 4, 0, stream_));
     check(zr_memcpy_async(count_.ptr, zi.data(), n_ * 4, 0, stream_));
+    check(zr_memcpy_async(dropped_.ptr, zi.data(), n_ * 4, 0, stream_));
     check(zr_stream_synchronize(stream_));  // the host vectors are pageable and go out of scope
     injected_.resize(n_);
 }
@@ -164,7 +168,7 @@ void DeviceHandTracker::step(const std::vector<Image> &frames, double now_ms) {
     // 2. bookkeeping (tracking.rs:129-218)
     check(zr_hand_manage_async(state_.ptr, ids_.ptr, hroi_.ptr, src_.ptr, nhands_.ptr, next_id_.ptr, next_det_.ptr,
                                det_pending_.ptr, count_.ptr, dets_.ptr, dcap_, fsize_.ptr, n_, &cfg_, now_ms,
-                               steps_ == 0 ? 1 : 0, views_.ptr, stream_));
+                               steps_ == 0 ? 1 : 0, views_.ptr, dropped_.ptr, stream_));
     // 3. the hand landmark network on every slot's view of this frame
     float *outs[4] = {outs_[0].ptr, outs_[1].ptr, outs_[2].ptr, outs_[3].ptr};
     const ColorMapper hc = hand_->color_mapper();
@@ -192,6 +196,21 @@ std::vector<int32_t> DeviceHandTracker::hand_counts() {
     return h;
 }
 
+std::vector<int32_t> DeviceHandTracker::dropped_hands() {
+    std::vector<int32_t> h(n_);
+    check(zr_memcpy_async(h.data(), dropped_.ptr, n_ * 4, 1, stream_));
+    synchronize();
+    return h;
+}
+
+std::vector<int32_t> DeviceHandTracker::dropped_detections() {
+    std::vector<int32_t> h(n_);
+    check(zr_memcpy_async(h.data(), count_.ptr, n_ * 4, 1, stream_));
+    synchronize();
+    for (auto &c : h) c = c > (int32_t)dcap_ ? c - (int32_t)dcap_ : 0;
+    return h;
+}
+
 std::vector<int32_t> DeviceHandTracker::detection_pending() {
     std::vector<int32_t> h(n_);
     check(zr_memcpy_async(h.data(), det_pending_.ptr, n_ * 4, 1, stream_));
@@ -203,12 +222,12 @@ std::vector<DeviceHandTracker::HandData> DeviceHandTracker::hands(size_t s) {
     if (s >= n_) throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "stream index out of range");
     const int H = cfg_.slots, L = hand_net_.num_landmarks;
     int32_t nh = 0;
-    std::vector<uint32_t> ids(H);
+    std::vector<uint64_t> ids(H);
     std::vector<int32_t> src(H);
     std::vector<float> roi(5 * H), lm((size_t)H * L * 3);
     std::vector<zr_track_state> st(H);
     check(zr_memcpy_async(&nh, nhands_.ptr + s, 4, 1, stream_));
-    check(zr_memcpy_async(ids.data(), ids_.ptr + s * H, 4 * H, 1, stream_));
+    check(zr_memcpy_async(ids.data(), ids_.ptr + s * H, 8 * H, 1, stream_));
     check(zr_memcpy_async(src.data(), src_.ptr + s * H, 4 * H, 1, stream_));
     check(zr_memcpy_async(roi.data(), hroi_.ptr + s * H * 5, 20 * H, 1, stream_));
     check(zr_memcpy_async(lm.data(), lm_out_.ptr + (size_t)s * H * L * 3, lm.size() * 4, 1, stream_));

@@ -41,7 +41,7 @@ class DeviceHandTracker {
     int slots() const { return cfg_.slots; }
 
     struct HandData {  // tracking.rs:237-262
-        uint32_t id;
+        uint64_t id;  // HandId(u64), tracking.rs:227
         std::vector<float> landmarks;  // 21 x 3, frame px (the previous step's estimate)
         RotatedRect view_rect;         // the hand's ROI
     };
@@ -49,6 +49,13 @@ class DeviceHandTracker {
     std::vector<HandData> hands(size_t s);
     std::vector<int32_t> hand_counts();  // every stream's hands, tracked or new
     std::vector<int32_t> detection_pending();  // streams whose palm detection of the last step counts
+    // per stream, the last step's new hands that found no free slot of the `slots` (the reference's
+    // hand list is unbounded, tracking.rs:158-194; here capacity is fixed and its overflow reported)
+    std::vector<int32_t> dropped_hands();
+    // per stream, palm detections of the last palm pass past the detection capacity (0: the
+    // capacity is the detector's anchor count, the most NMS can return)
+    std::vector<int32_t> dropped_detections();
+    size_t detection_capacity() const { return dcap_; }
 
   private:
     std::shared_ptr<const Cnn> palm_, hand_;
@@ -57,14 +64,15 @@ class DeviceHandTracker {
     zr_hand_cfg cfg_{};
     zr_track_cfg tcfg_{};
     zr_detpost_cfg pcfg_{};
-    size_t n_ = 0, dcap_ = 8;
+    size_t n_ = 0, dcap_ = 0;  // dcap_: every NMS output (the palm detector's anchor count)
     uint64_t steps_ = 0;
     void *stream_ = nullptr;
     uint32_t fw_ = 0, fh_ = 0;  // frame size the letterbox table was built for
     DeviceArray<zr_track_state> state_;
-    DeviceArray<uint32_t> ids_, next_id_, fsize_;
+    DeviceArray<uint64_t> ids_, next_id_;
+    DeviceArray<uint32_t> fsize_;
     DeviceArray<float> hroi_, lm_out_, outs_[4], palm_boxes_, palm_logits_, anchors_, lbox_, dets_;
-    DeviceArray<int32_t> src_, nhands_, det_pending_, count_;
+    DeviceArray<int32_t> src_, nhands_, det_pending_, count_, dropped_;
     DeviceArray<double> next_det_;
     DeviceArray<zr_view_desc> views_;
     std::vector<std::vector<Detection>> injected_;

@@ -105,7 +105,10 @@ DetectTrackPipeline::DetectTrackPipeline(PipelineConfig cfg, int device, int thr
     : cfg_(std::move(cfg)), device_(device), det_cnn_(network_cnn(cfg_.detector.kind, device)),
       lm_cnn_(network_cnn(cfg_.landmarker.kind, device)), pool_(threads) {
     nms_.set_iou_thresh(cfg_.nms_iou);
+    nms_.set_mode(cfg_.nms_mode);
     if (cfg_.device_post) {
+        // 0: the detector's anchor count, the most NMS can return (nothing dropped)
+        if (cfg_.det_cap == 0) cfg_.det_cap = (uint32_t)cfg_.detector.anchors().size();
         if (cfg_.det_cap < cfg_.max_rois_per_frame) cfg_.det_cap = cfg_.max_rois_per_frame;
         const auto &a = cfg_.detector.anchors();
         d_anchors_.resize(2 * a.size());
@@ -122,6 +125,8 @@ DetectTrackPipeline::DetectTrackPipeline(PipelineConfig cfg, int device, int thr
         else s.stream = stream_;
         check(zr_event_create(&s.ev_det));
         check(zr_event_create(&s.ev_lm));
+        check(zr_event_create(&s.ev_rec));
+        for (auto &e : s.ev_t) check(zr_event_create_timing(&e));
     }
 }
 
@@ -131,8 +136,75 @@ DetectTrackPipeline::~DetectTrackPipeline() {
         if (s->stream && s->stream != stream_) zr_stream_destroy(s->stream);
         if (s->ev_det) zr_event_destroy(s->ev_det);
         if (s->ev_lm) zr_event_destroy(s->ev_lm);
+        if (s->ev_rec) zr_event_destroy(s->ev_rec);
+        for (auto e : s->ev_t)
+            if (e) zr_event_destroy(e);
     }
+    if (gstream_) {
+        zr_stream_synchronize(gstream_);
+        zr_stream_destroy(gstream_);
+    }
+    for (auto e : ev_gath_)
+        if (e) zr_event_destroy(e);
     if (stream_) zr_stream_destroy(stream_);
+}
+
+size_t DetectTrackPipeline::det_cap() const { return cfg_.det_cap; }
+
+void DetectTrackPipeline::enable_records(uint32_t rmax, uint32_t first_id, uint32_t id_stride, zr_comm *comm,
+                                         int world) {
+    if (!cfg_.device_post) throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "device records need device post-processing");
+    if (rmax == 0 || rmax > 64 || world < 1 || (comm && world < 1))
+        throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "bad record configuration");
+    if (gstream_) check(zr_stream_synchronize(gstream_));
+    rec_rmax_ = rmax;
+    rec_first_ = first_id;
+    rec_stride_ = id_stride;
+    comm_ = comm;
+    world_ = comm ? world : 1;
+    // the gather runs on its own stream: with the sub-batch streams that is 4 hardware queues,
+    // the HIP default (GPU_MAX_HW_QUEUES), and the null stream stays idle in the steady state
+    if (!gstream_) check(zr_stream_create(&gstream_));
+    for (int k = 0; k < 2; k++) {
+        if (!ev_gath_[k]) check(zr_event_create(&ev_gath_[k]));
+        gath_used_[k] = false;
+    }
+}
+
+// every active slot has enqueued step enq_steps_ (its records into set enq_steps_ & 1): the gather
+// stream waits for their post-processing, all-gathers the set (with a communicator) and marks it
+void DetectTrackPipeline::enqueue_gather() {
+    if (!rec_rmax_) return;
+    const int set = (int)(enq_steps_ & 1);
+    for (size_t k = 0; k < active_slots_; k++) check(zr_stream_wait_event(gstream_, slots_[k]->ev_rec));
+    if (comm_) {
+        const size_t bytes = frames_.size() * record_width() * sizeof(float);
+        d_gath_[set].resize((size_t)world_ * frames_.size() * record_width());
+        check(zr_comm_all_gather_async(comm_, d_rec_[set].ptr, d_gath_[set].ptr, bytes, gstream_));
+    }
+    check(zr_event_record(ev_gath_[set], gstream_));
+    gath_used_[set] = true;
+    enq_steps_++;
+}
+
+std::vector<float> DetectTrackPipeline::records() {
+    if (!rec_rmax_ || done_steps_ == 0) throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "no finished step with records");
+    const int set = (int)((done_steps_ - 1) & 1);
+    check(zr_event_synchronize(ev_gath_[set]));
+    std::vector<float> out(frames_.size() * record_width());
+    check(zr_memcpy_async(out.data(), d_rec_[set].ptr, out.size() * 4, 1, nullptr));
+    check(zr_stream_synchronize(nullptr));
+    return out;
+}
+
+std::vector<float> DetectTrackPipeline::gathered() {
+    if (!comm_ || done_steps_ == 0) throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "no gathered step (no communicator)");
+    const int set = (int)((done_steps_ - 1) & 1);
+    check(zr_event_synchronize(ev_gath_[set]));
+    std::vector<float> out((size_t)world_ * frames_.size() * record_width());
+    check(zr_memcpy_async(out.data(), d_gath_[set].ptr, out.size() * 4, 1, nullptr));
+    check(zr_stream_synchronize(nullptr));
+    return out;
 }
 
 static double session_stat(const Cnn &c, bool flops) {
@@ -206,8 +278,12 @@ void DetectTrackPipeline::stage_detect(Slot &s, const std::vector<Image> &frames
     s.d_count.resize(n);
     s.d_rec.resize(n * cap * rec_w);
     float *douts[2] = {s.d_boxes.ptr, s.d_logits.ptr};
+    if (cfg_.device_post) check(zr_event_record(s.ev_t[0], s.stream));
     dc.estimate_async(s.zf, zv, vf, douts, s.stream);
-    if (cfg_.device_post) return;  // stage_device_post continues on the stream
+    if (cfg_.device_post) {  // stage_device_post continues on the stream
+        check(zr_event_record(s.ev_t[1], s.stream));
+        return;
+    }
     check(zr_detection_candidates_async(s.d_logits.ptr, s.d_boxes.ptr, (uint32_t)n, A, D,
                                         candidate_logit_floor(cfg_.det_threshold), cap, s.d_count.ptr,
                                         s.d_rec.ptr, s.stream));
@@ -300,12 +376,25 @@ void DetectTrackPipeline::stage_device_post(Slot &s, const std::vector<Image> &f
     pc.in_h = (int)dc.input_height();
     pc.thresh = cfg_.det_threshold;
     pc.iou = cfg_.nms_iou;
+    pc.mode = cfg_.nms_mode == SuppressionMode::Remove ? 1 : 0;
+    float *rec = nullptr;
+    const bool records = rec_rmax_ && &frames == &frames_;  // (records cover the resident frame set)
+    if (records) {  // this step's set of the all-gather records, frames f0 ..
+        const int set = (int)(enq_steps_ & 1);
+        d_rec_[set].resize(frames_.size() * record_width());
+        // the set's previous gather (two steps ago) must have read it before it is rewritten
+        if (gath_used_[set]) check(zr_stream_wait_event(s.stream, ev_gath_[set]));
+        rec = d_rec_[set].ptr + s.f0 * record_width();
+    }
     check(zr_detect_post_async(s.d_logits.ptr, s.d_boxes.ptr, d_anchors_.ptr, s.d_lbox.ptr, n, &pc, d_count,
-                               o.dets.ptr, dcap, nullptr, 0, 0, 1, s.stream));
+                               o.dets.ptr, dcap, rec, rec_rmax_, rec_first_ + (uint32_t)s.f0 * rec_stride_,
+                               rec_stride_, s.stream));
+    if (records) check(zr_event_record(s.ev_rec, s.stream));
     const zr_track_cfg tc = track_cfg();
     check(zr_track_seed_detections_async(d_count, o.dets.ptr, dcap, s.d_forced.ptr, s.d_nforced.ptr, s.d_fsize.ptr,
                                          n, &tc, cfg_.roi_grow, cfg_.roi_use_angle ? 1 : 0, d_state, d_seed,
                                          s.d_views.ptr, s.stream));
+    check(zr_event_record(s.ev_t[2], s.stream));
     float *lptr[4] = {nullptr, nullptr, nullptr, nullptr};
     for (size_t k = 0; k < nout && k < 4; k++) {
         o.lm[k].resize((size_t)lc.nn().output_per_image(k) * nv);
@@ -314,12 +403,15 @@ void DetectTrackPipeline::stage_device_post(Slot &s, const std::vector<Image> &f
     const ColorMapper cm = lc.color_mapper();
     check(zr_cnn_estimate_device_views_async(lc.nn().handle(), s.zf.data(), n, s.d_views.ptr, nv, cm.lo, cm.hi, lptr,
                                              s.stream));
+    check(zr_event_record(s.ev_t[3], s.stream));
     const bool flagged = tc.kind <= 2;
     check(zr_track_update_async(d_state, nv, &tc, lptr[0], (size_t)lc.nn().output_per_image(0),
                                 flagged ? lptr[1] : nullptr, flagged ? (size_t)lc.nn().output_per_image(1) : 0,
                                 o.lmout.ptr, s.d_views.ptr, s.stream));
+    check(zr_event_record(s.ev_t[4], s.stream));
     check(zr_memcpy_async(o.h_sum.ptr, o.sum.ptr, sum_bytes, 1, s.stream));
     check(zr_event_record(s.ev_lm, s.stream));
+    s.timed = true;
     s.wr ^= 1;  // the next step of this slot writes the other set
 }
 
@@ -329,7 +421,19 @@ void DetectTrackPipeline::finish_device(Slot &s) {
     const size_t n = s.nf, R = std::max(1u, cfg_.max_rois_per_frame), nv = n * R;
     const zr_track_state *st = reinterpret_cast<const zr_track_state *>(o.h_sum.ptr);
     const int32_t *cnt = reinterpret_cast<const int32_t *>(st + 2 * nv);
-    for (size_t i = 0; i < n; i++) times_.detections += (size_t)cnt[i];
+    for (size_t i = 0; i < n; i++) {
+        times_.detections += (size_t)cnt[i];
+        if ((size_t)cnt[i] > cfg_.det_cap) times_.dropped_detections += (size_t)cnt[i] - cfg_.det_cap;
+    }
+    if (s.timed) {  // the stage spans of this step on the slot's stream
+        float ms[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < 4; k++) check(zr_event_elapsed(&ms[k], s.ev_t[k], s.ev_t[k + 1]));
+        times_.detect_gpu_ms += ms[0];
+        times_.decode_nms_ms += ms[1];
+        times_.landmark_gpu_ms += ms[2];
+        times_.map_ms += ms[3];
+        s.timed = false;
+    }
     for (size_t v = 0; v < nv; v++) {
         times_.rois += st[nv + v].active ? 1 : 0;
         times_.tracked += st[v].tracked ? 1 : 0;
@@ -359,8 +463,12 @@ void DetectTrackPipeline::unpack_device(Slot &s) const {
     const zr_track_state *state = reinterpret_cast<const zr_track_state *>(o.h_sum.ptr);
     const zr_track_state *seed = state + nv;
     const int32_t *count = reinterpret_cast<const int32_t *>(seed + nv);
-    std::vector<float> dets(n * dcap * 20), lmout(nv * L * 3), extra[2];
-    check(zr_memcpy_async(dets.data(), o.dets.ptr, dets.size() * 4, 1, nullptr));
+    // only the rows that hold detections: dcap is the detector's whole output by default
+    int maxc = 0;
+    for (size_t i = 0; i < n; i++) maxc = std::max(maxc, std::min(count[i], (int32_t)dcap));
+    const size_t dw = (size_t)maxc;  // detections per frame in the host copy
+    std::vector<float> dets(std::max<size_t>(1, n * dw * 20)), lmout(nv * L * 3), extra[2];
+    check(zr_memcpy2d_async(dets.data(), dw * 80, o.dets.ptr, dcap * 80, dw * 80, n, 1, nullptr));
     check(zr_memcpy_async(lmout.data(), o.lmout.ptr, lmout.size() * 4, 1, nullptr));
     for (size_t k = 2; k < nout && k < 4; k++) {  // handedness / world landmarks / tongue_out
         extra[k - 2].resize((size_t)lc.nn().output_per_image(k) * nv);
@@ -373,7 +481,7 @@ void DetectTrackPipeline::unpack_device(Slot &s) const {
         auto &fd = dets_[f];
         fd.clear();
         for (int k = 0; k < cnt && k < (int)dcap; k++) {
-            const float *e = &dets[(i * dcap + k) * 20];
+            const float *e = &dets[(i * dw + k) * 20];
             Detection d;
             d.confidence = e[0];
             d.angle = e[1];
@@ -556,13 +664,15 @@ void DetectTrackPipeline::run(const std::vector<Image> &frames,
         if (cfg_.device_post) stage_device_post(s, frames, forced);
     }
     active_slots_ = S;
+    if (cfg_.device_post && rec_rmax_ && &frames == &frames_) enqueue_gather();
     for (size_t k = 0; k < S && cfg_.device_post; k++) {
         Slot &s = *slots_[k];
         const auto t = clk::now();
         check(zr_event_synchronize(s.ev_lm));
-        times_.landmark_gpu_ms += ms_since(t);
+        times_.host_wait_ms += ms_since(t);
         finish_device(s);
     }
+    if (cfg_.device_post) done_steps_ = enq_steps_;
     if (cfg_.device_post) {
         times_.total_ms = ms_since(t0);
         return;
@@ -594,6 +704,9 @@ void DetectTrackPipeline::run(const std::vector<Image> &frames,
 void DetectTrackPipeline::begin_steps() {
     steps_t0_ = clk::now();
     times_ = StageTimes{};
+    if (gstream_) check(zr_stream_synchronize(gstream_));
+    enq_steps_ = done_steps_ = 0;
+    gath_used_[0] = gath_used_[1] = false;
     const std::vector<Image> &frames = frames_;
     const size_t B = frames.size();
     active_slots_ = std::min<size_t>(slots_.size(), B);
@@ -607,6 +720,7 @@ void DetectTrackPipeline::begin_steps() {
         stage_detect(s, frames);
         if (cfg_.device_post) stage_device_post(s, frames, forced_);
     }
+    if (cfg_.device_post) enqueue_gather();
 }
 
 void DetectTrackPipeline::step(bool more) {
@@ -621,16 +735,16 @@ void DetectTrackPipeline::step(bool more) {
         Slot &s = *slots_[k];
         const auto t = clk::now();
         check(zr_event_synchronize(s.ev_lm));
-        times_.landmark_gpu_ms += ms_since(t);
-        const auto t1 = clk::now();
+        times_.host_wait_ms += ms_since(t);
         finish_device(s);
         if (more) {
             stage_detect(s, frames);
             stage_device_post(s, frames, forced_);
         }
-        times_.map_ms += ms_since(t1);
     }
     if (cfg_.device_post) {
+        done_steps_++;
+        if (more) enqueue_gather();
         times_.frames += B;
         times_.total_ms = ms_since(steps_t0_);
         return;

@@ -48,9 +48,18 @@ struct RoiResult {
     RotatedRect next_roi;  // valid when tracked
 };
 
-struct StageTimes {  // mirrors Detector::timers / Estimator::timers (detection.rs:273-275)
+// Mirrors Detector::timers / Estimator::timers (detection.rs:273-275, landmark.rs:289-291).
+// Host mode: the host's waits for each GPU stage and its own decode / map work.  Device mode:
+// HIP-event spans of each stage on the sub-batch streams, summed over the sub-batches (they run
+// concurrently, so the sum may exceed the wall time): detector inference, decode + NMS + map + ROI
+// seeding, landmark inference, tracker update; host_wait_ms is the host's wait for the steps.
+struct StageTimes {
     double detect_gpu_ms = 0, decode_nms_ms = 0, landmark_gpu_ms = 0, map_ms = 0, total_ms = 0;
+    double host_wait_ms = 0;
     size_t frames = 0, detections = 0, rois = 0, tracked = 0;
+    // detections past PipelineConfig::det_cap (device mode; 0 with the default cap, which keeps
+    // the detector's whole output)
+    size_t dropped_detections = 0;
 };
 
 struct PipelineConfig {
@@ -58,6 +67,7 @@ struct PipelineConfig {
     LandmarkNetwork landmarker = LandmarkNetwork::face_mesh_v1();
     float det_threshold = Detector::DEFAULT_THRESHOLD;
     float nms_iou = NonMaxSuppression::DEFAULT_IOU_THRESH;
+    SuppressionMode nms_mode = SuppressionMode::Average;  // Detector::nms_mut().set_mode
     // ROI from a detection: RotatedRect(det.rect.grow_rel(roi_grow), use_det_angle ? angle : 0)
     float roi_grow = 0.f;
     bool roi_use_angle = false;
@@ -75,10 +85,11 @@ struct PipelineConfig {
     // (zr_detect_post_async -> zr_track_seed_detections_async -> landmarks ->
     // zr_track_update_async, one stream per sub-batch, no host step in between); false = the
     // host restatement (decode/NMS/map and the tracker update on the thread pool).  Both give
-    // the same bits; device mode keeps the first det_cap detections of a frame (the count stays
-    // exact).
+    // the same bits.  det_cap: detections kept per frame on the device; 0 = the detector's anchor
+    // count, the most NMS can return, so nothing is ever dropped (the reference's Detections is a
+    // Vec, detection.rs:44-111).  A smaller cap counts what it drops in StageTimes.
     bool device_post = true;
-    uint32_t det_cap = 16;
+    uint32_t det_cap = 0;
     static PipelineConfig face();  // BlazeFace -> FaceMesh V1 (config 3)
     static PipelineConfig hand();  // BlazePalm lite -> hand landmark lite (config 4)
 };
@@ -128,12 +139,29 @@ class DetectTrackPipeline {
     void begin_steps();
     void step(bool more);
 
+    // every step's per-frame detection records ([B][2 + 20 rmax] f32: frame id
+    // first_id + f * id_stride, count, the first rmax detections) written on the device by the
+    // post-processing itself, and -- with a communicator -- all-gathered over the node's ranks on
+    // the pipeline's own stream, overlapping the next step.  No host copy on that path.
+    void enable_records(uint32_t rmax, uint32_t first_id, uint32_t id_stride, zr_comm *comm = nullptr,
+                        int world = 1);
+    uint32_t record_width() const { return 2 + 20 * rec_rmax_; }
+    // the last finished step's records of this rank (host copy, waits for them) ...
+    std::vector<float> records();
+    // ... and the gathered records of every rank ([world][B][W], needs a communicator)
+    std::vector<float> gathered();
+
   private:
     // one software-pipeline slot: a contiguous range of frames with its own stream/buffers
     struct Slot {
         size_t f0 = 0, nf = 0;
         void *stream = nullptr;
         void *ev_det = nullptr, *ev_lm = nullptr;  // stage-1 / stage-3 outputs on the host
+        // device mode: timing events around the stages (detector, post + seed, landmarks,
+        // update) and the event after this step's records were written
+        void *ev_t[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+        void *ev_rec = nullptr;
+        bool timed = false;
         DeviceArray<float> d_boxes, d_logits, d_rec, d_lm[4];
         DeviceArray<int32_t> d_count;
         PinnedArray<float> h_rec, h_lm[4];
@@ -174,6 +202,8 @@ class DetectTrackPipeline {
     void stage_decode_and_rois(Slot &s, const std::vector<Image> &frames,
                                const std::vector<std::vector<RotatedRect>> &forced);
     void stage_map(Slot &s);
+    void enqueue_gather();  // after every active slot enqueued a step (records on)
+    size_t det_cap() const;
 
     PipelineConfig cfg_;
     int device_;
@@ -191,6 +221,14 @@ class DetectTrackPipeline {
     std::vector<std::vector<RotatedRect>> forced_;
     size_t active_slots_ = 0;
     std::chrono::steady_clock::time_point steps_t0_;
+    // records (enable_records): two sets, step t writes set t & 1
+    uint32_t rec_rmax_ = 0, rec_first_ = 0, rec_stride_ = 1;
+    zr_comm *comm_ = nullptr;
+    int world_ = 1;
+    DeviceArray<float> d_rec_[2], d_gath_[2];
+    void *gstream_ = nullptr, *ev_gath_[2] = {nullptr, nullptr};
+    bool gath_used_[2] = {false, false};
+    uint64_t enq_steps_ = 0, done_steps_ = 0;
 };
 
 }  // namespace zh

@@ -128,7 +128,33 @@ __global__ __launch_bounds__(64) void det_post_kernel(const DetPostParams P) {
             __syncthreads();
         }
         rem = nk;
-        if (lane == 0) {
+        if (lane == 0 && P.mode == 1) {
+            // SuppressionMode::Remove (nms.rs:70-76): the group is dropped, the seed kept as decoded
+            const float *b = boxes + (int64_t)ca[seed] * P.D;
+            const Decoded d = decode(P, b, ca[seed]);
+            const float cxi = d.cx * (float)P.in_w, cyi = d.cy * (float)P.in_h;
+            float e[20];
+            e[0] = cc[seed];
+            e[1] = d.angle;
+            e[2] = d.cx * scale + tlx;
+            e[3] = d.cy * scale + tly;
+            e[4] = d.w * scale;
+            e[5] = d.h * scale;
+#pragma unroll
+            for (int k = 0; k < 7; ++k) {
+                e[6 + 2 * k] = k < P.nkp ? (b[4 + 2 * k] + cxi) * scale + tlx : 0.f;
+                e[7 + 2 * k] = k < P.nkp ? (b[5 + 2 * k] + cyi) * scale + tly : 0.f;
+            }
+            if (out < P.dcap) {
+                float *o = P.dets + ((int64_t)f * P.dcap + out) * 20;
+#pragma unroll
+                for (int k = 0; k < 20; ++k) o[k] = e[k];
+            }
+            if (rec && out < P.rmax) {
+#pragma unroll
+                for (int k = 0; k < 20; ++k) rec[2 + 20 * out + k] = e[k];
+            }
+        } else if (lane == 0) {
             // the weighted average over [seed] + group, each accumulator summed in that order
             float divisor = 0.f, ax = 0.f, ay = 0.f, aw = 0.f, ah = 0.f, aa = 0.f;
             float kx[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, ky[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};

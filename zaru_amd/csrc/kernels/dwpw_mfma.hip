@@ -422,321 +422,6 @@ void dwpw_dma_kernel(const DwPwParams P, int nct, int runmax, int bufsz) {
     for (int t = 0; t < MTW; ++t) epilogue_tile(G, acc[t], on, oq, m0 + (wm * MTW + t) * 32, kh);
 }
 
-// ------------------------------------------------------------------ persistent LDS-ring form
-// The low-resolution BlazeBlocks are a small GEMM (M, K <= 128..256) behind a depthwise
-// prologue, over many columns.  Per tile of BN columns the per-chunk form above pays a dependent
-// HBM round trip for every 16-channel chunk, re-stages the layer's 1x1 weights for every tile
-// (60 % of each chunk's LDS copy), fences its epilogue behind residual / bias loads, and runs
-// its depthwise and MFMA phases back to back.  Measured per phase (tools/debug):
-// MFMA busy < 25 %, and a tile's fixed costs (index math, barriers, epilogue) repeat per 8
-// chunks.  This form instead:
-//   * is persistent: one 512-thread workgroup per CU (8 waves, WM along M x 8/WM along N) walks
-//     a run of column tiles (contiguous runs per XCD, so halo rows are L2 hits);
-//   * stages the whole layer's 1x1 weights, depthwise weights / biases, the epilogue bias and
-//     the activation slopes in LDS once per workgroup;
-//   * streams the activation runs through a ring of D LDS stages by LDS-DMA, D - 1 chunks ahead
-//     across tile boundaries, waiting with a counted vmcnt for exactly the stage it needs (the
-//     DMA count per wave and stage is fixed, and nothing else in the loop loads to VGPRs);
-//   * software-pipelines the chunk loop: in one barrier interval the waves compute chunk g + 1's
-//     depthwise into one of two depthwise tiles while the MFMAs consume chunk g from the other;
-//   * takes the block's residual from the staged taps (the centre tap, or the 2x2 max-pool of
-//     the taps at stride 2) into a second pair of tiles, which the MFMA phase moves into the
-//     lanes' accumulator layout -- the epilogue reads no global memory.
-// Same arithmetic in the same order as dwpw_dma_kernel / dwpw_kernel: bitwise equal.
-constexpr int RING_DFKC = 16;
-
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate is a compile-time field)
-__device__ __forceinline__ void wait_vmcnt(int n) {
-    switch (__builtin_amdgcn_readfirstlane(n)) {
-#define ZR_VMW(i) case i: asm volatile("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
-        ZR_VMW(0) ZR_VMW(1) ZR_VMW(2) ZR_VMW(3) ZR_VMW(4) ZR_VMW(5) ZR_VMW(6) ZR_VMW(7)
-        ZR_VMW(8) ZR_VMW(9) ZR_VMW(10) ZR_VMW(11) ZR_VMW(12) ZR_VMW(13) ZR_VMW(14) ZR_VMW(15)
-        ZR_VMW(16) ZR_VMW(17) ZR_VMW(18) ZR_VMW(19) ZR_VMW(20) ZR_VMW(21) ZR_VMW(22) ZR_VMW(23)
-        ZR_VMW(24) ZR_VMW(25) ZR_VMW(26) ZR_VMW(27) ZR_VMW(28) ZR_VMW(29) ZR_VMW(30) ZR_VMW(31)
-        ZR_VMW(32) ZR_VMW(33) ZR_VMW(34) ZR_VMW(35) ZR_VMW(36) ZR_VMW(37) ZR_VMW(38) ZR_VMW(39)
-        ZR_VMW(40) ZR_VMW(41) ZR_VMW(42) ZR_VMW(43) ZR_VMW(44) ZR_VMW(45) ZR_VMW(46) ZR_VMW(47)
-        ZR_VMW(48) ZR_VMW(49) ZR_VMW(50) ZR_VMW(51) ZR_VMW(52) ZR_VMW(53) ZR_VMW(54) ZR_VMW(55)
-        ZR_VMW(56) ZR_VMW(57) ZR_VMW(58) ZR_VMW(59) ZR_VMW(60) ZR_VMW(61) ZR_VMW(62)
-#undef ZR_VMW
-    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
-    }
-}
-
-// activation of N values with their per-channel slopes in LDS (PReLU); same arithmetic as
-// apply_act_n, the uniform switch outside the element loop
-template <int N, typename ChanFn>
-__device__ __forceinline__ void ring_act_n(int kind, float lo, float hi, const float *slope, float *v, ChanFn ch) {
-    switch (kind) {
-    case ACT_RELU:
-#pragma unroll
-        for (int r = 0; r < N; ++r) v[r] = fmaxf(v[r], 0.f);
-        break;
-    case ACT_CLIP:
-#pragma unroll
-        for (int r = 0; r < N; ++r) v[r] = fminf(fmaxf(v[r], lo), hi);
-        break;
-    case ACT_PRELU:
-#pragma unroll
-        for (int r = 0; r < N; ++r) v[r] = v[r] < 0.f ? v[r] * slope[ch(r)] : v[r];
-        break;
-    case ACT_SIGMOID:
-#pragma unroll
-        for (int r = 0; r < N; ++r) v[r] = 1.f / (1.f + expf(-v[r]));
-        break;
-    default: break;
-    }
-}
-
-// Launch-time layout of one ring launch (host-computed, passed by value).
-struct RingPlan {
-    int nct;          // column tiles
-    int nch;          // channel chunks (RING_DFKC each)
-    int rq;           // 16-B slots per channel in a stage (the longest tile run)
-    int stg;          // floats per stage (whole 1 KiB DMA wave-instructions)
-    int D;            // ring depth
-    int tpx;          // tiles per XCD range
-    int res;          // residual from the staged taps: 0 none, 1 centre tap, 2 2x2 max-pool
-    // LDS offsets (floats)
-    int o_ring, o_w, o_dw, o_db, o_b, o_spre, o_spost, o_sdw, o_d, o_r, lds_floats;
-};
-
-template <int K, int S, int WM, bool RES>
-__global__ __launch_bounds__(512) void dwpw_ring_kernel(const DwPwParams P, const RingPlan R) {
-    constexpr int NW = 8, WN = NW / WM, BN = WN * 32, KK = K * K, FK = RING_DFKC;
-    constexpr int CPAR = 512 / BN, PER = FK / CPAR;
-    constexpr int PL = DwPad<K, S>::L;  // the residual taps (the host checks the pads are these)
-    static_assert(PER >= 1 && FK % CPAR == 0, "tile / chunk mismatch");
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const GemmParams &G = P.g;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int kh = lane >> 5, col = lane & 31;
-    const int wm = wave % WM, wn = wave / WM;
-
-    // this workgroup's tiles: XCD x owns tiles [x * tpx, (x + 1) * tpx); its G8 workgroups take
-    // them round robin
-    const int G8 = gridDim.x >> 3, xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-    const int t_beg = xcd * R.tpx + slot, t_end = min((xcd + 1) * R.tpx, R.nct);
-    const int ntl = t_beg < t_end ? (t_end - t_beg + G8 - 1) / G8 : 0;
-    if (ntl == 0) return;  // whole workgroup, before any barrier
-    const int nstages = ntl * R.nch;
-    const int Cin = G.K, H = P.in.H, W = P.in.W, Pin = H * W, OW = P.OW, Pq = G.P;
-    const int pt = P.pad_t, pl = P.pad_l, Mpad = G.Mpad, rs4 = R.rq * 4;
-    const float inv_pq = 1.f / (float)Pq, inv_ow = 1.f / (float)OW, inv_rq = 1.f / (float)R.rq;
-    float *ring = lds + R.o_ring, *sW = lds + R.o_w, *sDW = lds + R.o_dw, *sDB = lds + R.o_db;
-    float *sB = lds + R.o_b, *sPre = lds + R.o_spre, *sPost = lds + R.o_spost, *sDS = lds + R.o_sdw;
-    float *sD = lds + R.o_d, *sR = lds + R.o_r;
-    constexpr int DS = BN;  // depthwise-tile row stride
-
-    // ---- once per workgroup: weights, depthwise parameters, bias and slopes into LDS
-    {
-        const int kr = R.nch * FK;  // weight rows staged (rows >= Kpad are zero)
-        const int m4 = Mpad / 4, n4 = kr * m4;
-        for (int i = tid; i < n4; i += 512) {
-            const int k = i / m4, m = 4 * (i - k * m4);
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (k < G.Kpad) v = *reinterpret_cast<const float4 *>(G.wt + (size_t)k * Mpad + m);
-            *reinterpret_cast<float4 *>(sW + 4 * i) = v;
-        }
-        for (int i = tid; i < kr * KK; i += 512) sDW[i] = i < Cin * KK ? P.dw_w[i] : 0.f;
-        for (int i = tid; i < kr; i += 512) {
-            sDB[i] = i < Cin ? P.dw_b[i] : 0.f;
-            sDS[i] = (P.dw_act.kind == ACT_PRELU && i < Cin) ? P.dw_act.slope[i] : 0.f;
-        }
-        for (int i = tid; i < Mpad; i += 512) {
-            sB[i] = G.bias[i];
-            sPre[i] = (G.pre.kind == ACT_PRELU && i < G.M) ? G.pre.slope[i] : 0.f;
-            sPost[i] = (G.post.kind == ACT_PRELU && i < G.M) ? G.post.slope[i] : 0.f;
-        }
-    }
-
-    // the input run of tile t: first float (16-B aligned, from a channel's base) and length / 4
-    auto run_of = [&](int t, int &s0, int &run4) {
-        const int ja = t * BN, jb = min(ja + BN, G.ncols) - 1;
-        const int na = qdiv(ja, Pq, inv_pq), qa = ja - na * Pq, nb = qdiv(jb, Pq, inv_pq), qb = jb - nb * Pq;
-        const int ya = max(qdiv(qa, OW, inv_ow) * S - pt, 0), yb = min(qdiv(qb, OW, inv_ow) * S - pt + K - 1, H - 1);
-        s0 = (na * Pin + ya * W) & ~3;
-        run4 = (((nb * Pin + (yb + 1) * W + 3) & ~3) - s0) >> 2;
-    };
-
-    // ---- the DMA side: stages in (tile, chunk) order, D - 1 ahead of the compute side
-    const int nwi = R.stg >> 8;                                      // wave-instructions per stage
-    const int cnt_w = wave < nwi ? (nwi - wave + NW - 1) / NW : 0;  // of them issued by this wave
-    int i_tile = t_beg, i_chunk = 0, i_s0 = 0, i_run4 = 0, i_slot = 0, issued = 0;
-    run_of(i_tile, i_s0, i_run4);
-    auto issue_next = [&]() {
-        const int kc = i_chunk * FK;
-        float *dst = ring + i_slot * R.stg;
-        for (int wi = wave; wi < nwi; wi += NW) {
-            const int sl = wi * 64 + lane;
-            const int c = qdiv(sl, R.rq, inv_rq), i = sl - c * R.rq;
-            const float *src = (const float *)&zr_zero4;
-            if (c < FK && kc + c < Cin && i < i_run4)
-                src = P.in.p + (size_t)(uint32_t)(kc + c) * (uint32_t)P.in.sC + (uint32_t)(i_s0 + 4 * i);
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                             (__attribute__((address_space(3))) void *)(dst + wi * 256), 16, 0, 0);
-        }
-        ++issued;
-        i_slot = i_slot + 1 == R.D ? 0 : i_slot + 1;
-        if (++i_chunk == R.nch) {
-            i_chunk = 0;
-            i_tile += G8;
-            if (i_tile < t_end) run_of(i_tile, i_s0, i_run4);
-        }
-    };
-
-    // ---- the depthwise side (stage g + 1 while the MFMAs take stage g): column dj of the tile,
-    // channels dc + CPAR * i of each chunk
-    const int dj = tid % BN;
-    int dc = tid / BN;
-    if constexpr (BN >= 64) dc = __builtin_amdgcn_readfirstlane(dc);  // one channel per wave
-    int d_tile = t_beg - G8, d_chunk = R.nch - 1, d_slot = 0, d_tb = 0;
-    uint32_t d_mask = 0;
-    auto d_advance = [&]() {  // to the next stage; a new tile's per-thread tap geometry
-        if (++d_chunk == R.nch) {
-            d_chunk = 0;
-            d_tile += G8;
-            int s0, run4;
-            run_of(d_tile, s0, run4);
-            const int jd = min(d_tile * BN + dj, G.ncols - 1);
-            const int n = qdiv(jd, Pq, inv_pq), qq = jd - n * Pq;
-            const int oy = qdiv(qq, OW, inv_ow), ox = qq - oy * OW;
-            const int iy0 = oy * S - pt, ix0 = ox * S - pl;
-            d_tb = n * Pin + iy0 * W + ix0 - s0;
-            d_mask = 0;
-#pragma unroll
-            for (int ky = 0; ky < K; ++ky)
-#pragma unroll
-                for (int kx = 0; kx < K; ++kx) {
-                    const int iy = iy0 + ky, ix = ix0 + kx;
-                    d_mask |= (iy >= 0 && iy < H && ix >= 0 && ix < W ? 1u : 0u) << (ky * K + kx);
-                }
-        }
-    };
-    float x[PER][KK];
-    auto d_load = [&]() {  // this thread's taps of the current depthwise stage
-        const float *stage = ring + d_slot * R.stg + d_tb;
-#pragma unroll
-        for (int i = 0; i < PER; ++i)
-#pragma unroll
-            for (int ky = 0; ky < K; ++ky)
-#pragma unroll
-                for (int kx = 0; kx < K; ++kx) x[i][ky * K + kx] = stage[(dc + CPAR * i) * rs4 + ky * W + kx];
-    };
-    auto d_compute = [&](int db) {  // depthwise (+ residual taps) of the loaded taps into tile db
-        const int kc = d_chunk * FK;
-        float dv[PER];
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int c = kc + dc + CPAR * i;
-            const float *w = sDW + c * KK;
-            float a = sDB[c];
-#pragma unroll
-            for (int t = 0; t < KK; ++t) a = __builtin_fmaf(w[t], ((d_mask >> t) & 1u) ? x[i][t] : 0.f, a);
-            dv[i] = a;
-        }
-        ring_act_n<PER>(P.dw_act.kind, P.dw_act.lo, P.dw_act.hi, sDS, dv, [&](int i) {
-            const int c = kc + dc + CPAR * i;
-            return c < Cin ? c : Cin - 1;
-        });
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int c = kc + dc + CPAR * i;
-            sD[db * FK * DS + (dc + CPAR * i) * DS + dj] = c < Cin ? dv[i] : 0.f;
-            if constexpr (RES) {
-                float r;
-                if constexpr (S == 1) {
-                    r = x[i][PL * K + PL];
-                } else {
-                    r = fmaxf(fmaxf(x[i][PL * K + PL], x[i][PL * K + PL + 1]),
-                              fmaxf(x[i][(PL + 1) * K + PL], x[i][(PL + 1) * K + PL + 1]));
-                }
-                sR[db * FK * DS + (dc + CPAR * i) * DS + dj] = c < G.r_C ? r : 0.f;
-            }
-        }
-        d_slot = d_slot + 1 == R.D ? 0 : d_slot + 1;
-    };
-
-    // ---- prologue: parameters visible, first D stages in flight, chunk 0's depthwise
-    while (issued < R.D && issued < nstages) issue_next();
-    __syncthreads();  // the parameter stores (and, through vmcnt(0), the whole first ring)
-    d_advance();
-    d_load();
-    d_compute(0);
-
-    f32x16 acc;
-    float rv[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f, rv[r] = 0.f;
-    const int mb = wm * 32;  // this wave's 32 output channels
-    int c_tile = t_beg, c_chunk = 0;
-
-    for (int g = 0; g < nstages; ++g) {
-        const bool more = g + 1 < nstages;
-        // stage g + 1 has landed (this wave's part: the later stages may stay in flight) ...
-        if (more) wait_vmcnt((issued - (g + 2)) * cnt_w);
-        // ... for every wave; every wave is done with chunk g - 1 (its slot and tile buffers)
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (issued < nstages) issue_next();  // into the slot chunk g's depthwise read
-        if (more) d_advance();
-
-        // chunk g's MFMAs interleaved with chunk g + 1's depthwise (independent tile buffers)
-        const int kc = c_chunk * FK;
-        const float *bD = sD + (g & 1) * FK * DS + wn * 32 + col, *bW = sW + (size_t)kc * Mpad + mb + col;
-        float av[FK / 2], bv[FK / 2];
-#pragma unroll
-        for (int s = 0; s < FK / 2; ++s) {
-            av[s] = bW[(2 * s + kh) * Mpad];
-            bv[s] = bD[(2 * s + kh) * DS];
-        }
-        // (after the last chunk this recomputes a stale stage into the idle tile buffer: no
-        // branch, so the scheduler can interleave the two instruction streams)
-        d_load();
-#pragma unroll
-        for (int s = 0; s < FK / 2; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
-        d_compute((g + 1) & 1);
-#pragma unroll
-        for (int s = 0; s < FK / 2; ++s) {  // 1 MFMA, then a share of the depthwise VALU / LDS work
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 2 + PER * KK / (FK / 2), 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 2 + (PER * KK * 2) / (FK / 2), 0);
-        }
-        if constexpr (RES) {  // the chunk's residual rows of this wave's accumulator rows
-            const float *bR = sR + (g & 1) * FK * DS + wn * 32 + col;
-            if (kc == mb) {
-#pragma unroll
-                for (int r = 0; r < 8; ++r) rv[r] = bR[mfma32_row(r, kh) * DS];
-            } else if (kc == mb + 16) {
-#pragma unroll
-                for (int r = 8; r < 16; ++r) rv[r] = bR[(mfma32_row(r, kh) - 16) * DS];
-            }
-        }
-        if (++c_chunk == R.nch) {  // the tile's last chunk: epilogue (bias, act, residual, act, store)
-            c_chunk = 0;
-            const int j = c_tile * BN + wn * 32 + col;
-            c_tile += G8;
-            if (j < G.ncols) {
-                const int n = qdiv(j, Pq, inv_pq), q = j - n * Pq;
-                const uint32_t ob = (uint32_t)n * (uint32_t)G.o_sN + (uint32_t)q * (uint32_t)G.o_sP;
-                float v[16];
-                auto chan = [&](int r) { return mb + mfma32_row(r, kh); };
-#pragma unroll
-                for (int r = 0; r < 16; ++r) v[r] = acc[r] + sB[chan(r)];
-                ring_act_n<16>(G.pre.kind, G.pre.lo, G.pre.hi, sPre, v, chan);
-                if constexpr (RES) {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) v[r] += rv[r];
-                }
-                ring_act_n<16>(G.post.kind, G.post.lo, G.post.hi, sPost, v, chan);
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    if (chan(r) < G.M) G.out[ob + (uint32_t)chan(r) * (uint32_t)G.o_sC] = v[r];
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0.f, rv[r] = 0.f;
-        }
-    }
-}
-
 namespace {
 
 struct DwPwLayout {
@@ -840,103 +525,12 @@ const char *dwpw_layout(const DwPwParams &p, const DwPwLayout &l, hipStream_t s)
     }
 }
 
-// The ring form's plan for one launch, or nullptr when it does not apply: a single M tile
-// (Mpad <= 256), a CNHW input with 16-B aligned channel planes, a residual that is the block
-// input (or none), and the weights, parameters and a ring of >= 2 stages within the LDS.
-template <int K, int S, int WM>
-static const char *ring_go(const DwPwParams &p, hipStream_t s) {
-    constexpr int BN = (8 / WM) * 32, BM = WM * 32, FK = RING_DFKC, KK = K * K;
-    const GemmParams &g = p.g;
-    const int H = p.in.H, W = p.in.W, Pin = H * W, Pq = g.P, OW = p.OW, OH = g.P / p.OW;
-    if (p.in.sN != Pin || p.in.sC % 4 || ((uintptr_t)p.in.p | (uintptr_t)g.wt) % 16 || g.Mpad % 4 ||
-        g.Mpad > BM || p.pad_t * W + p.pad_l > 256)
-        return nullptr;
-    int res = 0;
-    if (g.res_mode != 0) {
-        const int PL = DwPad<K, S>::L;
-        if (g.r != p.in.p || g.r_sN != p.in.sN || g.r_sC != p.in.sC || g.r_C > g.K || p.pad_t != PL ||
-            p.pad_l != PL)
-            return nullptr;
-        if (g.res_mode == 1 && S == 1 && OW == W && OH == H) res = 1;
-        else if (g.res_mode == 2 && S == 2 && g.r_W == W && H % 2 == 0 && W % 2 == 0 && 2 * OW == W &&
-                 2 * OH == H && PL + 1 < K)
-            res = 2;
-        else
-            return nullptr;
-    }
-    RingPlan R{};
-    R.nct = (g.ncols + BN - 1) / BN;
-    R.nch = (g.K + FK - 1) / FK;
-    int rm = 0;
-    for (int j0 = 0; j0 < g.ncols; j0 += BN) {  // tiles repeat with the image period
-        const int jb = std::min(j0 + BN, g.ncols) - 1;
-        const int na = j0 / Pq, qa = j0 - na * Pq, nb = jb / Pq, qb = jb - nb * Pq;
-        const int ya = std::max(qa / OW * S - p.pad_t, 0), yb = std::min(qb / OW * S - p.pad_t + K - 1, H - 1);
-        const int s0 = (na * Pin + ya * W) & ~3, e0 = (nb * Pin + (yb + 1) * W + 3) & ~3;
-        rm = std::max(rm, e0 - s0);
-        if (na >= 4 && (j0 % Pq) == 0) break;
-    }
-    R.rq = rm / 4;
-    R.stg = (FK * R.rq + 63) / 64 * 256;
-    R.res = res;
-    const int kr = R.nch * FK, bm = std::max(g.Mpad, BM);
-    // fixed part (floats): guard, weights, depthwise weights / biases / slopes, bias and slopes,
-    // two depthwise tiles (+ two residual tiles)
-    const int fixed = 256 + kr * g.Mpad + (kr * KK + 3) / 4 * 4 + 2 * kr + 3 * bm + 2 * FK * BN * (res ? 2 : 1);
-    const int budget = 160 * 1024 / 4;
-    const int D = std::min(8, (budget - fixed) / R.stg);
-    if (D < 2) return nullptr;
-    R.D = D;
-    R.o_ring = 256;
-    R.o_w = R.o_ring + D * R.stg;
-    R.o_dw = R.o_w + kr * g.Mpad;
-    R.o_db = R.o_dw + (kr * KK + 3) / 4 * 4;
-    R.o_sdw = R.o_db + kr;
-    R.o_b = R.o_sdw + kr;
-    R.o_spre = R.o_b + bm;
-    R.o_spost = R.o_spre + bm;
-    R.o_d = R.o_spost + bm;
-    R.o_r = R.o_d + 2 * FK * BN;
-    R.lds_floats = R.o_r + (res ? 2 * FK * BN : 0);
-    static const int ncu = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-        return n;
-    }();
-    const int G = (std::min(R.nct, ncu) + 7) / 8 * 8;
-    R.tpx = (R.nct + 7) / 8;
-    static const bool attr = [] {
-        return hipFuncSetAttribute((const void *)dwpw_ring_kernel<K, S, WM, false>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess &&
-               hipFuncSetAttribute((const void *)dwpw_ring_kernel<K, S, WM, true>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-    }();
-    (void)attr;
-    const size_t lds = sizeof(float) * (size_t)R.lds_floats;
-    if (res) hipLaunchKernelGGL((dwpw_ring_kernel<K, S, WM, true>), dim3(G), dim3(512), lds, s, p, R);
-    else hipLaunchKernelGGL((dwpw_ring_kernel<K, S, WM, false>), dim3(G), dim3(512), lds, s, p, R);
-    return kernel_name("dwpw_ring_kernel<%d,%d,%d,%s>", K, S, WM, res ? "true" : "false");
-}
-
-template <int K, int S>
-static const char *ring_launch(const DwPwParams &p, hipStream_t s) {
-    if (p.g.Mpad <= 64) return ring_go<K, S, 2>(p, s);
-    if (p.g.Mpad <= 128) return ring_go<K, S, 4>(p, s);
-    return ring_go<K, S, 8>(p, s);
-}
-
 }  // namespace
 
 // Layout choice for the MFMA forms: no M split unless Mpad > 256, at most 1/3 padded rows;
 // among those, the widest column tile that still gives >= 4 workgroups per CU (else the most
 // workgroups).
 const char *launch_dwpw_mfma(const DwPwParams &p, hipStream_t s) {
-    if (form_on(FORM_RING) && p.g.Mpad <= 256) {
-        const char *k = p.k == 3 ? (p.stride == 1 ? ring_launch<3, 1>(p, s) : ring_launch<3, 2>(p, s))
-                                 : (p.stride == 1 ? ring_launch<5, 1>(p, s) : ring_launch<5, 2>(p, s));
-        if (k) return k;
-    }
     // workgroups one launch should reach (ZARU_HIP_MINWGS overrides it for layout sweeps)
     static const int64_t min_wgs = [] {
         const char *e = std::getenv("ZARU_HIP_MINWGS");

@@ -128,7 +128,11 @@ __global__ __launch_bounds__(64) void jpeg_huff_kernel(const JpegHuffParams P) {
     int pred[3] = {0, 0, 0};
     bool bad = false;
     const int m0 = iv * F.restart, m1 = min(m0 + F.restart, F.nmcu);
-    for (int m = m0; m < m1 && !bad; m++) {
+    // Every block of the interval is written, also after a corrupt symbol: from the first bad
+    // code on, the rest of the interval gets all-zero blocks (libjpeg's insufficient-data rule:
+    // jdhuff.c zeroes the MCU and skips decoding), so no block keeps a previous frame's
+    // coefficients from the reused buffer.  The frame's error flag reports it.
+    for (int m = m0; m < m1; m++) {
         const int my = m / F.mcux, mx = m - my * F.mcux;
         for (int c = 0; c < F.ncomp; c++) {
             const JpegHuffTable &dc = T[F.td[c]], &ac = T[4 + F.ta[c]];
@@ -142,6 +146,7 @@ __global__ __launch_bounds__(64) void jpeg_huff_kernel(const JpegHuffParams P) {
                         F.coef + (F.coef_off[c] + (int64_t)by * F.bw[c] + bx) * 64);
 #pragma unroll
                     for (int z = 0; z < 8; z++) mine[z] = make_int4(0, 0, 0, 0);
+                    const bool was_bad = bad;
                     {  // DC: category, then that many magnitude bits
                         const uint32_t w = win.at(bp);
                         const uint32_t e = dc.lk[w >> 23] & 0xFFFFu;
@@ -153,7 +158,7 @@ __global__ __launch_bounds__(64) void jpeg_huff_kernel(const JpegHuffParams P) {
                         bad |= !ok;
                         pred[c] += ok && sc ? extend(bits_after(w, len, sc), sc) : 0;
                         bp += len + (ok ? sc : 0);
-                        co[0] = (int16_t)pred[c];
+                        co[0] = was_bad ? (int16_t)0 : (int16_t)pred[c];
                     }
                     // AC, branch-free per symbol (lanes decode different data, so every branch
                     // would be taken by some lane): the fast entry and the long-code search are
@@ -182,7 +187,7 @@ __global__ __launch_bounds__(64) void jpeg_huff_kernel(const JpegHuffParams P) {
                 }
         }
     }
-    if (bad) *P.error = 1;
+    if (bad) P.error[P.wg[2 * blockIdx.x]] = 1;  // per frame of the call
 }
 
 }  // namespace

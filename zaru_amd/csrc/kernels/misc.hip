@@ -27,8 +27,8 @@ const char *kernel_name(const char *fmt, ...) {
 
 bool form_on(Form f) {
     static const unsigned mask = [] {
-        static const char *const names[FORM_COUNT] = {"dma", "v4", "valu", "valu_db", "rows", "chain", "vres", "vstore", "ring", "ir"};
-        unsigned m = ((1u << FORM_COUNT) - 1) & ~(1u << FORM_CHAIN) & ~(1u << FORM_RING) & ~(1u << FORM_IR);  // opt-in: chain, ring, ir
+        static const char *const names[FORM_COUNT] = {"dma", "v4", "valu", "valu_db", "rows", "vres", "vstore"};
+        unsigned m = (1u << FORM_COUNT) - 1;
         const char *e = std::getenv("ZARU_HIP_FORMS");
         for (std::string s = e ? e : ""; !s.empty();) {
             const size_t comma = s.find(',');

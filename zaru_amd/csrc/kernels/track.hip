@@ -251,19 +251,22 @@ __global__ __launch_bounds__(64) void hand_manage_kernel(const HandManageParams 
         const int j = base + k;
         float r[5];
         for (int c = 0; c < 5; ++c) r[c] = st.tracked ? st.updated[c] : P.hroi[i * 5 + c];
-        const uint32_t id = P.ids[i];
+        const uint64_t id = P.ids[i];
         P.state[j] = st;
         P.ids[j] = id;
         P.src[j] = h;
         for (int c = 0; c < 5; ++c) P.hroi[j * 5 + c] = r[c];
         ++k;
     }
-    // 2./3. the previous step's palm detections: keep those whose grown box overlaps no hand,
-    // then start a hand for each kept one (RotatedRect(grow_rel(1.5), angle), LandmarkTracker::set_roi)
+    // 2./3. the previous step's palm detections: keep those whose grown box overlaps no hand
+    // that existed before this step's new ones (Vec::retain over self.hands, tracking.rs:140-156),
+    // then start a hand for each kept one (RotatedRect(grow_rel(1.5), angle), LandmarkTracker::
+    // set_roi, 158-194).  Every detection is visited (dcap is the detector's whole output); a
+    // kept detection with no free slot left is counted in `dropped` (the reference's Vec grows)
+    int dropped = 0;
     if (P.det_pending[s]) {
         const int cnt = min(P.count[s], P.dcap);
         const int k0 = k;
-        uint32_t keep = 0;  // dcap <= 32
         for (int d = 0; d < cnt; ++d) {
             const float *dd = P.dets + ((int64_t)s * P.dcap + d) * 20;
             const RRect g = grow_rel({dd[2], dd[3], dd[4], dd[5], 0.f}, P.grow);
@@ -272,12 +275,11 @@ __global__ __launch_bounds__(64) void hand_manage_kernel(const HandManageParams 
                 const float *r = P.hroi + (base + j) * 5;
                 ok = iou(r[0], r[1], r[2], r[3], g.cx, g.cy, g.w, g.h) < P.iou;
             }
-            keep |= (ok ? 1u : 0u) << d;
-        }
-        for (int d = 0; d < cnt; ++d) {
-            if (!((keep >> d) & 1u) || k >= P.H) continue;  // past H slots: dropped (capacity)
-            const float *dd = P.dets + ((int64_t)s * P.dcap + d) * 20;
-            const RRect g = grow_rel({dd[2], dd[3], dd[4], dd[5], 0.f}, P.grow);
+            if (!ok) continue;
+            if (k >= P.H) {  // capacity: reported, never silent
+                ++dropped;
+                continue;
+            }
             const int j = base + k;
             TrackState st{};
             st.roi[0] = g.cx;
@@ -295,6 +297,7 @@ __global__ __launch_bounds__(64) void hand_manage_kernel(const HandManageParams 
             ++k;
         }
     }
+    if (P.dropped) P.dropped[s] = dropped;
     // 4. for i in (0..len).rev(): the first earlier hand it overlaps removes it by swap_remove
     for (int i = k - 1; i >= 0; --i) {
         const float *a = P.hroi + (base + i) * 5;

@@ -272,7 +272,8 @@ struct zr_jpeg_decoder {
     // bytes staged in pinned memory and copied once per frame
     uint8_t *h_stage = nullptr, *d_stage = nullptr;
     size_t stage_cap = 0;
-    int *d_err = nullptr;         // set by jpeg_huff_kernel on a corrupt interval
+    int *d_err = nullptr;         // [4096] per frame of the last call: set by jpeg_huff_kernel on a corrupt interval
+    size_t n_last = 0;            // frames of the last call
     uint64_t n_gpu = 0, n_host = 0;
     hipEvent_t staged = nullptr;  // the last H2D copy out of h_coef / h_stage has completed
     hipEvent_t done = nullptr;    // the last decode's kernels (readers of d_coef / d_planes) completed
@@ -453,7 +454,8 @@ int zr_jpeg_decoder_create(int device, zr_jpeg_decoder **out) {
             delete d;
             return err(ZR_ERR_DEVICE, "hipEventCreate failed");
         }
-        if (hipMalloc((void **)&d->d_err, sizeof(int)) != hipSuccess || hipMemset(d->d_err, 0, sizeof(int)) != hipSuccess) {
+        if (hipMalloc((void **)&d->d_err, 4096 * sizeof(int)) != hipSuccess ||
+            hipMemset(d->d_err, 0, 4096 * sizeof(int)) != hipSuccess) {
             (void)hipEventDestroy(d->staged);
             (void)hipEventDestroy(d->done);
             delete d;
@@ -488,12 +490,30 @@ int zr_jpeg_decoder_status(zr_jpeg_decoder *d, uint64_t *gpu_entropy, uint64_t *
         if (gpu_entropy) *gpu_entropy = d->n_gpu;
         if (host_entropy) *host_entropy = d->n_host;
         if (corrupt) {
-            int e = 0;
+            int e[4096];
+            const size_t n = d->n_last;
             if (hipSetDevice(d->device) != hipSuccess || hipEventSynchronize(d->done) != hipSuccess ||
-                hipMemcpy(&e, d->d_err, sizeof e, hipMemcpyDeviceToHost) != hipSuccess)
+                (n && hipMemcpy(e, d->d_err, n * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess))
                 return err(ZR_ERR_DEVICE, "jpeg: status read failed");
-            *corrupt = e;
+            *corrupt = 0;
+            for (size_t f = 0; f < n; f++) *corrupt |= e[f] ? 1 : 0;
         }
+        return ZR_OK;
+    } catch (...) {
+        return err(ZR_ERR_INTERNAL, "jpeg: internal error");
+    }
+}
+
+int zr_jpeg_frame_errors(zr_jpeg_decoder *d, int32_t *flags, size_t cap, size_t *n) {
+    try {
+        if (!d || !n) return err(ZR_ERR_INVALID_ARGUMENT, "null argument");
+        std::lock_guard<std::mutex> g(d->mu);
+        *n = d->n_last;
+        if (!flags) return ZR_OK;
+        if (cap < d->n_last) return err(ZR_ERR_INVALID_ARGUMENT, "jpeg: flag buffer smaller than the last call");
+        if (hipSetDevice(d->device) != hipSuccess || hipEventSynchronize(d->done) != hipSuccess ||
+            (d->n_last && hipMemcpy(flags, d->d_err, d->n_last * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess))
+            return err(ZR_ERR_DEVICE, "jpeg: status read failed");
         return ZR_OK;
     } catch (...) {
         return err(ZR_ERR_INTERNAL, "jpeg: internal error");
@@ -717,6 +737,10 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
         if (n_wg && hipMemcpyAsync(dec->d_stage, dec->h_stage, used, hipMemcpyHostToDevice, st) != hipSuccess)
             return err(ZR_ERR_DEVICE, "jpeg: scan upload failed");
         if (hipEventRecord(dec->staged, st) != hipSuccess) return err(ZR_ERR_DEVICE, "jpeg: event record failed");
+        // this call's per-frame error flags (the device decode reports corruption asynchronously)
+        if (hipMemsetAsync(dec->d_err, 0, n * sizeof(int), st) != hipSuccess)
+            return err(ZR_ERR_DEVICE, "jpeg: flag reset failed");
+        dec->n_last = n;
         if (n_wg) {
             zr::JpegHuffParams hp{};
             hp.frames = reinterpret_cast<const zr::JpegHuffFrame *>(dec->d_stage);

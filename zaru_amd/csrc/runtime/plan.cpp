@@ -83,9 +83,6 @@ class Compiler {
     bool act_from_node(const OnnxNode &nd, int C, int Cpad, ActDesc &a);
     void finalize_outputs();
     void allocate();
-    void mark_inverted_residuals();
-    void schedule_sinks();
-    void form_chains();
 };
 
 // ---------------------------------------------------------------- shape inference
@@ -822,7 +819,7 @@ bool Compiler::lower() {
                 Step *prod = nullptr;
                 for (auto &st : P.steps)
                     if (st.out.kind == 0 && st.out.id == x.tensor) prod = &st;
-                if (!prod || prod->kind == S_CHAIN || prod->out.C * prod->out.H * prod->out.W != C)
+                if (!prod || prod->out.C * prod->out.H * prod->out.W != C)
                     return fail("Concat member " + in_name + " has no retargetable producer");
                 for (auto &st : P.steps)
                     if ((st.in.kind == 0 && st.in.id == x.tensor) || (st.in2.kind == 0 && st.in2.id == x.tensor))
@@ -853,46 +850,17 @@ bool Compiler::lower() {
     return true;
 }
 
-// Expand 1x1 -> (depthwise -> 1x1) pairs whose expanded tensor nothing else reads: run_plan may
-// launch them as one inverted-residual kernel (ir.hip), the expanded tensor never stored.
-void Compiler::mark_inverted_residuals() {
-    std::vector<int> reads(P.storage_size.size(), 0);
-    for (const Step &s : P.steps) {
-        for (const TRef *r : {&s.in, &s.in2})
-            if (r->kind == 0 && r->id >= 0) reads[r->id]++;
-        for (const TRef &r : s.chain_outs)
-            if (r.kind == 0 && r.id >= 0) reads[r.id]++;
-    }
-    for (size_t i = 0; i + 1 < P.steps.size(); i++) {
-        Step &e = P.steps[i];
-        const Step &d = P.steps[i + 1];
-        e.ir_next = e.kind == S_GEMM && e.KK == 1 && e.res_mode == 0 && e.out.kind == 0 && e.out.c_off == 0 &&
-                    e.in.kind == 0 && e.in.c_off == 0 && d.kind == S_DWPW && d.in.kind == 0 &&
-                    d.in.id == e.out.id && d.in.c_off == 0 && reads[e.out.id] == 1 && e.M == d.K;
-    }
-}
-
 void Compiler::allocate() {
     // liveness over step indices
     const size_t ns = P.storage_size.size();
     std::vector<int> first(ns, 1 << 30), last(ns, -1);
     for (size_t i = 0; i < P.steps.size(); i++) {
         const Step &s = P.steps[i];
-        std::vector<const TRef *> refs = {&s.in, &s.in2, &s.out};
-        for (const TRef &r : s.chain_outs) refs.push_back(&r);
-        for (const TRef *r : refs)
+        for (const TRef *r : {&s.in, &s.in2, &s.out})
             if (r->kind == 0 && r->id >= 0) {
                 first[r->id] = std::min(first[r->id], (int)i);
                 last[r->id] = std::max(last[r->id], (int)i);
             }
-    }
-    // a fused inverted residual (ir_next) reads the expand's input and writes the projection in
-    // ONE launch: the two must not share memory, so each is live across both steps
-    for (size_t i = 0; i + 1 < P.steps.size(); i++) {
-        if (!P.steps[i].ir_next) continue;
-        const TRef &x = P.steps[i].in, &o = P.steps[i + 1].out;
-        if (x.kind == 0 && x.id >= 0) last[x.id] = std::max(last[x.id], (int)i + 1);
-        if (o.kind == 0 && o.id >= 0) first[o.id] = std::min(first[o.id], (int)i);
     }
     std::vector<int> order(ns);
     for (size_t i = 0; i < ns; i++) order[i] = (int)i;
@@ -920,309 +888,6 @@ void Compiler::allocate() {
         placed.push_back(id);
     }
     P.arena_per_image = round_up(arena, 64);
-}
-
-// ---------------------------------------------------------------- layer chains
-namespace {
-
-constexpr int kChainMaxOps = 24, kChainLdsFloats = 40960;  // 160 KiB per workgroup
-constexpr int kChainKC = 16;
-
-int64_t positions(const TRef &r) { return (int64_t)r.H * r.W; }
-
-// a step the chain kernel can run: depthwise 3x3 -> 1x1 blocks and plain 1x1 convs over
-// <= 256 positions and <= 128 channels, reading internal tensors only
-bool chain_step_ok(const Step &s) {
-    if (s.in.kind != 0 || (s.res_mode && s.in2.kind != 0) || s.out.kind == 1) return false;
-    // chain.hip's epilogue activations are branch-free Relu / PRelu / Clip / none
-    if (s.pre.kind == ACT_SIGMOID || s.post.kind == ACT_SIGMOID || s.dw_act.kind == ACT_SIGMOID) return false;
-    if (positions(s.in) > 256 || positions(s.out) > 256 || s.M > 128 || s.K > 128) return false;
-    if (s.kind == S_DWPW) return s.kh == 3 && s.kw == 3 && (s.stride == 1 || s.stride == 2);
-    if (s.kind == S_GEMM) return s.KK == 1 && s.in.H == s.out.H && s.in.W == s.out.W;
-    return false;
-}
-
-int round4(int64_t v) { return (int)((v + 3) / 4 * 4); }
-
-}  // namespace
-
-// A step that writes only a graph output feeds nothing else.  Chainable ones move up to just
-// after the producer of their inputs (so the tensor they read dies sooner), the others move to
-// the end (so they do not split a run of chainable layers).
-void Compiler::schedule_sinks() {
-    std::vector<Step> &S = P.steps;
-    std::vector<Step> body, late;
-    for (auto &s : S) {
-        if (s.out.kind == 2 && !chain_step_ok(s)) late.push_back(s);
-        else body.push_back(s);
-    }
-    std::vector<Step> out;
-    std::vector<Step> pending;  // chainable sinks waiting for their inputs' producers
-    auto produced = [&](int id) {
-        for (auto &t : out)
-            if (t.out.kind == 0 && t.out.id == id) return true;
-        return false;
-    };
-    auto ready = [&](const Step &s) {
-        return (s.in.kind != 0 || produced(s.in.id)) && (!s.res_mode || s.in2.kind != 0 || produced(s.in2.id));
-    };
-    for (auto &s : body) {
-        if (s.out.kind == 2) {
-            if (ready(s)) {
-                // insert right after the last producer of its inputs
-                size_t pos = 0;
-                for (size_t i = 0; i < out.size(); i++)
-                    if (out[i].out.kind == 0 && (out[i].out.id == s.in.id || (s.res_mode && out[i].out.id == s.in2.id)))
-                        pos = i + 1;
-                out.insert(out.begin() + pos, s);
-            } else {
-                pending.push_back(s);
-            }
-            continue;
-        }
-        out.push_back(s);
-    }
-    for (auto &s : pending) out.push_back(s);
-    for (auto &s : late) out.push_back(s);
-    S = std::move(out);
-}
-
-// Replace every maximal run (>= 2 steps) of chainable steps whose activations fit in LDS by
-// one S_CHAIN step.  LDS: the entry tensor and every tensor produced and consumed inside the
-// run get bordered planes ((H+2) x (W+2) per channel) by liveness; a layer may write over the
-// tensors it consumes last (chain.hip stores after a barrier).  Tensors consumed after the run,
-// and graph outputs, are written to their global homes.
-void Compiler::form_chains() {
-    std::vector<Step> &S = P.steps;
-    auto plane = [](const TRef &r) { return (int64_t)(r.H + 2) * (r.W + 2); };
-    struct Alloc {
-        std::vector<int> off;      // per op: out region (-1: none)
-        std::map<int, int> where;  // storage id -> LDS offset
-        int end = 0, e_off = 0;
-        bool ok = false;
-    };
-    // LDS layout of steps [i, j] with entry tensor `entry`
-    auto layout = [&](size_t i, size_t j, const TRef &entry) {
-        Alloc A;
-        std::map<int, int> last;  // storage id -> last op index reading it within [i, j]
-        for (size_t k = i; k <= j; k++) {
-            last[S[k].in.id] = (int)k;
-            if (S[k].res_mode) last[S[k].in2.id] = (int)k;
-        }
-        struct Reg {
-            int off, size, id;
-        };
-        std::vector<Reg> live;
-        auto place = [&](int size, int prefer) {
-            std::sort(live.begin(), live.end(), [](const Reg &a, const Reg &b) { return a.off < b.off; });
-            auto fits = [&](int o) {
-                for (auto &r : live)
-                    if (o < r.off + r.size && r.off < o + size) return false;
-                return true;
-            };
-            if (prefer >= 0 && fits(prefer)) return prefer;
-            int o = 0;
-            for (auto &r : live) {
-                if (o + size <= r.off) break;
-                o = std::max(o, r.off + r.size);
-            }
-            return o;
-        };
-        auto release = [&](int id) {
-            live.erase(std::remove_if(live.begin(), live.end(), [&](const Reg &r) { return r.id == id; }), live.end());
-        };
-        const int esz = round4((int64_t)entry.C * plane(entry));
-        live.push_back({0, esz, entry.id});
-        A.where[entry.id] = 0;
-        A.end = esz;
-        for (size_t k = i; k <= j; k++) {
-            const Step &s = S[k];
-            if (!A.where.count(s.in.id) || (s.res_mode && !A.where.count(s.in2.id))) return A;  // not in LDS
-            bool used_later = false;
-            if (s.out.kind == 0)
-                for (size_t t = k + 1; t <= j; t++)
-                    if (S[t].in.id == s.out.id || (S[t].res_mode && S[t].in2.id == s.out.id)) used_later = true;
-            // inputs read for the last time may be overwritten by this layer's output
-            const int prefer = last[s.in.id] == (int)k ? A.where[s.in.id] : -1;
-            for (auto it = last.begin(); it != last.end(); ++it)
-                if (it->second == (int)k) release(it->first);
-            int off = -1;
-            if (used_later) {
-                const int sz = round4((int64_t)s.M * plane(s.out));
-                off = place(sz, prefer);
-                live.push_back({off, sz, s.out.id});
-                A.where[s.out.id] = off;
-                A.end = std::max(A.end, off + sz);
-            }
-            A.off.push_back(off);
-        }
-        A.ok = true;
-        return A;
-    };
-    auto d_stride = [](const Step &s) {
-        const int np = (int)((positions(s.out) + 15) / 16 * 16);
-        return np % 32 == 16 ? np : np + 16;
-    };
-    // consumer tiling: CHAIN_CONSUMER_WAVES waves as MS groups along M x (waves / MS) along N,
-    // MTW x NTW 16x16 tiles each, from the tilings chain.hip is instantiated for; fewest tiles
-    // per wave
-    struct Tiling {
-        int ms = 0, mtw = 0, ntw = 0;
-    };
-    auto tiling = [](const Step &s) {
-        Tiling best;
-        const int MT = (s.M + 15) / 16, NT = (int)((positions(s.out) + 15) / 16);
-        constexpr int CW = CHAIN_CONSUMER_WAVES;
-        for (int ms : {1, 2, 4, 8})
-            for (const auto &tl : CHAIN_TILINGS) {
-                const int mtw = tl[0], ntw = tl[1];
-                if (ms * mtw < MT || (CW / ms) * ntw < NT) continue;
-                if (!best.ms || mtw * ntw < best.mtw * best.ntw) best = Tiling{ms, mtw, ntw};
-            }
-        return best;
-    };
-    auto mpad_of = [&](const Step &s) {
-        const Tiling t = tiling(s);
-        return std::max(s.Mpad, t.ms * t.mtw * 16);
-    };
-    // per-layer parameters staged in LDS (chain.hip): bias, pre / post PReLU slopes [Mpad],
-    // depthwise channel records [Cin][12]
-    auto param_floats = [&](const Step &s) { return round4(3 * (int64_t)mpad_of(s) + 12 * (int64_t)s.K); };
-    // (chain.hip stages a layer's parameters with 2 per thread: <= 2048 floats)
-    auto step_ok = [&](const Step &s) { return chain_step_ok(s) && tiling(s).ms > 0 && param_floats(s) <= 2048; };
-
-    std::vector<Step> out;
-    for (size_t i = 0; i < S.size();) {
-        const Step &s0 = S[i];
-        const bool entry_ok = step_ok(s0);
-        size_t best_j = i;
-        Alloc best;
-        if (entry_ok) {
-            for (size_t j = i; j < S.size() && j - i < (size_t)kChainMaxOps && step_ok(S[j]); j++) {
-                Alloc A = layout(i, j, s0.in);
-                if (!A.ok) break;
-                int dmax = 0, pmax = 0;
-                for (size_t k = i; k <= j; k++) {
-                    if (S[k].kind == S_DWPW) dmax = std::max(dmax, d_stride(S[k]));
-                    pmax = std::max(pmax, param_floats(S[k]));
-                }
-                if (A.end + 2 * kChainKC * dmax + 2 * pmax > kChainLdsFloats) break;
-                best_j = j;
-                best = A;
-            }
-        }
-        if (!entry_ok || best_j - i < 1) {
-            out.push_back(S[i]);
-            i++;
-            continue;
-        }
-        // steps [i, best_j] become one chain
-        Step c;
-        c.kind = S_CHAIN;
-        c.name = "chain(" + S[i].name + " .. " + S[best_j].name + ")";
-        c.in = s0.in;
-        int dmax = 0, pmax = 0;
-        for (size_t k = i; k <= best_j; k++) {
-            if (S[k].kind == S_DWPW) dmax = std::max(dmax, d_stride(S[k]));
-            pmax = std::max(pmax, param_floats(S[k]));
-        }
-        c.chain_e_off = best.e_off;
-        c.chain_d_off = (best.end + 3) / 4 * 4;
-        c.chain_d_buf = kChainKC * dmax;
-        c.chain_p_off = c.chain_d_off + 2 * c.chain_d_buf;
-        c.chain_p_buf = pmax;
-        c.chain_lds = c.chain_p_off + 2 * c.chain_p_buf;
-        c.bytes = 4.0 * (double)s0.in.C * positions(s0.in);
-        std::vector<ChainOp> ops;
-        for (size_t k = i; k <= best_j; k++) {
-            const Step &s = S[k];
-            auto ref_of_id = [&](int id) -> TRef {  // geometry of an LDS tensor
-                if (id == s0.in.id) return s0.in;
-                for (size_t t = i; t < k; t++)
-                    if (S[t].out.kind == 0 && S[t].out.id == id) return S[t].out;
-                return TRef{};
-            };
-            const Tiling tl = tiling(s);
-            const int mpad = mpad_of(s), kpad = (s.K + kChainKC - 1) / kChainKC * kChainKC;
-            ChainOp o{};
-            o.kind = s.kind == S_DWPW ? CHAIN_DWPW : CHAIN_PW;
-            o.in_off = best.where[s.in.id];
-            o.res_off = s.res_mode ? best.where[s.in2.id] : -1;
-            o.out_off = best.off[k - i];
-            o.Cin = s.K;
-            o.Cout = s.M;
-            o.W = s.in.W;
-            o.OP = (int)positions(s.out);
-            o.OW = s.out.W;
-            const TRef rin = ref_of_id(s.in.id);
-            o.in_ps = (int)plane(rin);
-            o.in_wp = rin.W + 2;
-            o.out_ps = (int)plane(s.out);
-            o.out_wp = s.out.W + 2;
-            if (s.res_mode) {
-                const TRef rr = ref_of_id(s.in2.id);
-                o.res_ps = (int)plane(rr);
-                o.res_wp = rr.W + 2;
-            }
-            o.stride = s.stride;
-            o.pad_t = s.pad_t;
-            o.pad_l = s.pad_l;
-            o.Mpad = mpad;
-            o.MS = tl.ms;
-            o.MTW = tl.mtw;
-            o.NTW = tl.ntw;
-            o.NT = (o.OP + 15) / 16;
-            o.res_mode = s.res_mode;
-            o.r_C = s.r_C;
-            // zero-padded copies: 1x1 weights [kpad][mpad] (whole 16-row chunks, every wave's
-            // columns), bias and slopes [mpad]
-            std::vector<float> wt((size_t)kpad * mpad, 0.f), bias(mpad, 0.f);
-            for (int kk = 0; kk < s.K; kk++)
-                for (int m = 0; m < s.M; m++) wt[(size_t)kk * mpad + m] = P.weights[s.w_off + (size_t)kk * s.Mpad + m];
-            for (int m = 0; m < s.M; m++) bias[m] = P.weights[s.b_off + m];
-            o.w_off = (int)push_weights(wt);
-            o.b_off = (int)push_weights(bias);
-            o.dw_w_off = (int)s.dw_w_off;
-            o.dw_b_off = (int)s.dw_b_off;
-            auto act = [&](const ActDesc &a, int n) {
-                ChainAct r{a.kind, a.lo, a.hi, -1};
-                if (a.kind == ACT_PRELU) {
-                    std::vector<float> sl(n, 0.f);
-                    for (int m = 0; m < std::min(n, s.kind == S_DWPW && &a == &s.dw_act ? s.K : s.M); m++)
-                        sl[m] = P.weights[a.slope_off + m];
-                    r.slope_off = (int)push_weights(sl);
-                }
-                return r;
-            };
-            o.pre = act(s.pre, mpad);
-            o.post = act(s.post, mpad);
-            o.dw_act = act(s.dw_act, s.K);
-            o.ds = s.kind == S_DWPW ? d_stride(s) : 0;
-            o.zero_border = 1;
-            // a global destination: graph outputs, and internal tensors read after the chain
-            bool exported = false;
-            if (s.out.kind == 0)
-                for (size_t t = best_j + 1; t < S.size(); t++)
-                    if (S[t].in.id == s.out.id || (S[t].res_mode && S[t].in2.id == s.out.id)) exported = true;
-            o.gout = -1;
-            if (s.out.kind == 2 || exported) {
-                if (c.chain_outs.size() >= (size_t)CHAIN_MAX_OUTS) return;
-                o.gout = (int)c.chain_outs.size();
-                c.chain_outs.push_back(s.out);
-                c.bytes += 4.0 * (double)s.M * positions(s.out);
-            }
-            if (o.out_off < 0) o.zero_border = 0;
-            ops.push_back(o);
-            c.flops += s.flops;
-        }
-        std::vector<float> words(ops.size() * sizeof(ChainOp) / 4);
-        std::memcpy(words.data(), ops.data(), ops.size() * sizeof(ChainOp));
-        c.chain_ops_off = push_weights(words);
-        c.chain_nops = (int)ops.size();
-        out.push_back(c);
-        i = best_j + 1;
-    }
-    S = std::move(out);
 }
 
 bool Compiler::run(const std::vector<uint32_t> &sel) {
@@ -1270,17 +935,10 @@ bool Compiler::run(const std::vector<uint32_t> &sel) {
             for (auto &i : M.nodes[ni].in)
                 if (!i.empty()) vals[i].consumers++;
     if (!lower()) return false;
-    if (form_on(FORM_CHAIN)) {  // opt-in (ZARU_HIP_FORMS=+chain): see DESIGN.md
-        schedule_sinks();
-        form_chains();
-    }
     for (size_t oi = 0; oi < P.outputs.size(); oi++) {
         bool written = false;
-        for (auto &s : P.steps) {
+        for (auto &s : P.steps)
             if (s.out.kind == 2 && s.out.id == (int)oi) written = true;
-            for (auto &r : s.chain_outs)
-                if (r.kind == 2 && r.id == (int)oi) written = true;
-        }
         if (!written) return fail("output " + P.outputs[oi].name + " is never written");
     }
     for (auto &s : P.steps) {
@@ -1296,7 +954,6 @@ bool Compiler::run(const std::vector<uint32_t> &sel) {
                 reader = (int)i;
             }
     P.input_fusable = readers == 1 && P.steps[reader].kind == S_DIRECT && P.steps[reader].stem;
-    mark_inverted_residuals();
     allocate();
     return true;
 }
@@ -1449,20 +1106,7 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook
         if (hook) hook->before(stream);
         switch (s.kind) {
         case S_GEMM: {
-            const GemmParams g = gemm_of(s);
-            if (s.ir_next && si + 1 < plan.steps.size()) {  // expand + depthwise + project, one launch
-                IrParams ir{};
-                ir.e = g;
-                ir.d = dwpw_of(plan.steps[si + 1]);
-                if (const char *k = launch_ir(ir, stream)) {
-                    const Step &n = plan.steps[si + 1];
-                    if (hook) hook->after(stream, k, (s.bytes + n.bytes - 8.0 * s.M * s.out.H * s.out.W) * b.N,
-                                          (s.flops + n.flops) * b.N);
-                    ++si;
-                    continue;
-                }
-            }
-            kname = launch_gemm(g, stream);
+            kname = launch_gemm(gemm_of(s), stream);
             break;
         }
         case S_DWPW: {
@@ -1562,32 +1206,6 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook
             r.scale_y = s.scale_y;
             r.scale_x = s.scale_x;
             kname = launch_resize(r, stream);
-            break;
-        }
-        case S_CHAIN: {
-            ChainParams c{};
-            c.weights = W;
-            c.ops_off = (int)s.chain_ops_off;
-            c.nops = s.chain_nops;
-            Resolved e = resolve(s.in, plan, b);
-            c.entry = e.p;
-            c.e_sN = e.sN;
-            c.e_sC = e.sC;
-            c.e_C = s.in.C;
-            c.e_H = s.in.H;
-            c.e_W = s.in.W;
-            c.e_off = s.chain_e_off;
-            c.N = b.N;
-            c.d_off = s.chain_d_off;
-            c.d_buf = s.chain_d_buf;
-            c.p_off = s.chain_p_off;
-            c.p_buf = s.chain_p_buf;
-            c.lds_floats = s.chain_lds;
-            for (size_t i = 0; i < s.chain_outs.size(); i++) {
-                Resolved o = resolve(s.chain_outs[i], plan, b);
-                c.gout[i] = ChainOut{const_cast<float *>(o.p), o.sN, o.sC, o.sP};
-            }
-            kname = launch_chain(c, stream);
             break;
         }
         case S_GAP: {

@@ -18,7 +18,7 @@
 
 namespace zr {
 
-enum StepKind { S_GEMM, S_DW, S_DIRECT, S_ELT, S_RESIZE, S_GAP, S_DWPW, S_CHAIN };
+enum StepKind { S_GEMM, S_DW, S_DIRECT, S_ELT, S_RESIZE, S_GAP, S_DWPW };
 
 struct TRef {
     int kind = 0;  // 0 internal storage, 1 graph input, 2 graph output
@@ -52,16 +52,6 @@ struct Step {
     ActDesc dw_act;
     // S_DIRECT: runs as stem_kernel (Cin = 3, weights padded to 32 output channels)
     bool stem = false;
-    // S_GEMM: a plain 1x1 expand whose output only the next step (an S_DWPW) reads -- the pair
-    // may run as one inverted-residual launch (ir.hip); run_plan falls back to two launches
-    bool ir_next = false;
-    // S_CHAIN: a run of layers fused into one launch (chain.hip).  `in` is the entry tensor;
-    // the op table (ChainOp words) sits in the weight buffer at chain_ops_off; chain_outs are
-    // the global destinations the ops' `gout` index (exports of internal tensors, graph outputs)
-    int64_t chain_ops_off = -1;
-    int chain_nops = 0;
-    std::vector<TRef> chain_outs;
-    int chain_e_off = 0, chain_d_off = 0, chain_d_buf = 0, chain_p_off = 0, chain_p_buf = 0, chain_lds = 0;
     // algorithmic traffic / work per image (for roofline accounting); bytes_pre: the same
     // step sampling its input from RGBA frames (4 B per input pixel instead of 12)
     double bytes = 0, flops = 0, bytes_pre = 0;

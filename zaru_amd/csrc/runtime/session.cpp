@@ -201,9 +201,9 @@ struct zr_session {
         if (pool.size() < 8) {
             auto c = std::make_unique<Ctx>();
             (void)hipSetDevice(device);
-            if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-                hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess)
-                return nullptr;
+            // (the private stream is created on first use by a synchronous entry point: the async
+            // ones run on the caller's stream, and an idle stream still takes a hardware queue)
+            if (hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess) return nullptr;
             c->mu.lock();
             pool.push_back(std::move(c));
             return pool.back().get();
@@ -261,6 +261,12 @@ int enqueue(zr_session *s, Ctx *c, int N, const float *input, int64_t in_sN, int
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->done, stream));
+    return ZR_OK;
+}
+
+// the context's private stream (synchronous entry points only)
+int ctx_stream(Ctx *c) {
+    if (!c->stream) HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     return ZR_OK;
 }
 
@@ -407,12 +413,6 @@ int zr_plan_describe(const uint8_t *onnx, size_t len, const uint32_t *out_sel, s
             t += line;
         }
         for (auto &st : plan.steps) {
-            if (st.kind == zr::S_CHAIN) {
-                snprintf(line, sizeof line, "chain in=%s ops=%d outs=%zu lds_floats=%d flops/img=%.0f bytes/img=%.0f\n",
-                         ref(st.in).c_str(), st.chain_nops, st.chain_outs.size(), st.chain_lds, st.flops, st.bytes);
-                t += line;
-                continue;
-            }
             snprintf(line, sizeof line,
                      "%s%s in=%s out=%s k=%dx%d s=%d M=%d K=%d KK=%d pre=%s post=%s res=%d rC=%d elt=%d off=%lld oN=%lld oC=%lld oP=%lld in2=%s\n",
                      kinds[st.kind], st.stem ? " stem" : "", ref(st.in).c_str(), ref(st.out).c_str(), st.kh, st.kw, st.stride,
@@ -522,6 +522,7 @@ int zr_session_run(zr_session *s, size_t batch, const float *const *inputs, size
         HIP_TRY(hipSetDevice(s->device));
         const int64_t hw = (int64_t)s->plan.in_H * s->plan.in_W;
         const size_t in_floats = (size_t)hw * s->plan.in_C * batch;
+        if (int rc = ctx_stream(c)) return rc;
         if (int rc = grow(c->input, c->input_floats, in_floats)) return rc;
         if (int rc = sync_outputs(s, c, batch)) return rc;
         HIP_TRY(hipMemcpyAsync(c->input, inputs[0], in_floats * 4, hipMemcpyHostToDevice, c->stream));
@@ -665,7 +666,7 @@ int zr_detect_post_async(const float *d_logits, const float *d_boxes, const floa
         if (n == 0) return ZR_OK;
         if (cfg->anchors <= 0 || cfg->keypoints < 3 || cfg->keypoints > 7 ||
             cfg->params < 4 + 2 * cfg->keypoints || cfg->in_w <= 0 || cfg->in_h <= 0 || n > (1u << 24) ||
-            dcap > 4096 || rmax > 64 || (d_records && rmax == 0))
+            dcap > 65536 || rmax > 64 || (d_records && rmax == 0) || cfg->mode < 0 || cfg->mode > 1)
             return set_err(ZR_ERR_INVALID_ARGUMENT, "bad detection post-processing configuration");
         zr::DetPostParams p{};
         p.logits = d_logits;
@@ -681,6 +682,7 @@ int zr_detect_post_async(const float *d_logits, const float *d_boxes, const floa
         p.in_h = cfg->in_h;
         p.thresh = cfg->thresh;
         p.iou = cfg->iou;
+        p.mode = cfg->mode;
         p.count = d_count;
         p.dets = d_dets;
         p.dcap = (int)dcap;
@@ -730,17 +732,17 @@ int zr_track_seed_detections_async(const int32_t *d_count, const float *d_dets, 
     });
 }
 
-int zr_hand_manage_async(zr_track_state *d_state, uint32_t *d_ids, float *d_hroi, int32_t *d_src, int32_t *d_nhands,
-                         uint32_t *d_next_id, double *d_next_det, int32_t *d_det_pending, const int32_t *d_count,
+int zr_hand_manage_async(zr_track_state *d_state, uint64_t *d_ids, float *d_hroi, int32_t *d_src, int32_t *d_nhands,
+                         uint64_t *d_next_id, double *d_next_det, int32_t *d_det_pending, const int32_t *d_count,
                          const float *d_dets, size_t dcap, const uint32_t *d_frame_size, size_t n,
                          const zr_hand_cfg *cfg, double now_ms, int init_clock, zr_view_desc *d_views,
-                         void *hip_stream) {
+                         int32_t *d_dropped, void *hip_stream) {
     return guarded([&]() -> int {
         if (!d_state || !d_ids || !d_hroi || !d_src || !d_nhands || !d_next_id || !d_next_det || !d_det_pending ||
             !d_count || !d_dets || !d_frame_size || !cfg || !d_views)
             return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument");
         if (n == 0) return ZR_OK;
-        if (cfg->slots <= 0 || cfg->slots > 64 || dcap == 0 || dcap > 32 || (uint64_t)n * cfg->slots > (1u << 24) ||
+        if (cfg->slots <= 0 || cfg->slots > 64 || dcap == 0 || dcap > 65536 || (uint64_t)n * cfg->slots > (1u << 24) ||
             cfg->aspect_w <= 0 || cfg->aspect_h <= 0 || !(cfg->interval_ms >= 0.0) || !(cfg->palm_grow >= 0.f))
             return set_err(ZR_ERR_INVALID_ARGUMENT, "bad hand tracker configuration");
         zr::HandManageParams p{};
@@ -750,6 +752,7 @@ int zr_hand_manage_async(zr_track_state *d_state, uint32_t *d_ids, float *d_hroi
         p.src = d_src;
         p.nhands = d_nhands;
         p.next_id = d_next_id;
+        p.dropped = d_dropped;
         p.next_det = d_next_det;
         p.det_pending = d_det_pending;
         p.count = d_count;
@@ -823,6 +826,7 @@ int zr_cnn_estimate_views(zr_session *s, const uint8_t *rgba, uint32_t w, uint32
         CtxLock lk(c);
         HIP_TRY(hipSetDevice(s->device));
         const size_t bytes = row_stride * h;
+        if (int rc = ctx_stream(c)) return rc;
         if (int rc = grow(c->image, c->image_bytes, bytes ? bytes : 4)) return rc;
         if (int rc = sync_outputs(s, c, n_views)) return rc;
         HIP_TRY(hipStreamWaitEvent(c->stream, c->done, 0));
@@ -950,6 +954,40 @@ int zr_memcpy_async(void *dst, const void *src, size_t bytes, int kind, void *hi
         hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost
                                                                         : hipMemcpyDeviceToDevice;
         HIP_TRY(hipMemcpyAsync(dst, src, bytes, k, (hipStream_t)hip_stream));
+        return ZR_OK;
+    });
+}
+
+int zr_memcpy2d_async(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t height,
+                      int kind, void *hip_stream) {
+    return guarded([&]() -> int {
+        if (height == 0 || width == 0) return ZR_OK;
+        hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost
+                                                                        : hipMemcpyDeviceToDevice;
+        HIP_TRY(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, k, (hipStream_t)hip_stream));
+        return ZR_OK;
+    });
+}
+
+int zr_event_create_timing(void **event) {
+    return guarded([&]() -> int {
+        if (!event) return set_err(ZR_ERR_INVALID_ARGUMENT, "null event");
+        HIP_TRY(hipEventCreateWithFlags((hipEvent_t *)event, hipEventDefault));
+        return ZR_OK;
+    });
+}
+
+int zr_event_elapsed(float *ms, void *start, void *end) {
+    return guarded([&]() -> int {
+        if (!ms) return set_err(ZR_ERR_INVALID_ARGUMENT, "null ms");
+        HIP_TRY(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end));
+        return ZR_OK;
+    });
+}
+
+int zr_stream_wait_event(void *stream, void *event) {
+    return guarded([&]() -> int {
+        HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0));
         return ZR_OK;
     });
 }

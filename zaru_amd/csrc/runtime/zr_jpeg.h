@@ -60,7 +60,7 @@ struct JpegHuffParams {
     const JpegHuffFrame *frames;
     const int32_t *wg;            // [n_wg][2]
     int n_wg;
-    int *error;                   // set to 1 on a corrupt interval (bad code / AC index)
+    int *error;                   // [frame of the call] set to 1 on a corrupt interval (bad code / AC index)
     int lds_bytes;                // dynamic LDS: the largest 64-interval range, 16-B words + 1
 };
 int jpeg_huff_max_lds();          // the most dynamic LDS one workgroup may stage

@@ -178,84 +178,16 @@ struct DwPwParams {
     Act dw_act;
 };
 
-// MobileNetV2 inverted residual (ir.hip): the expand 1x1 conv `e` (x = block input) feeding the
-// depthwise -> 1x1 projection `d` (d.in describes the expanded plane: C = e.M, the input's H x W),
-// in one launch; th x tw output tiles (host-chosen by launch_ir).
-struct IrParams {
-    GemmParams e;
-    DwPwParams d;
-    int th, tw, tiles_x, tiles_y;
-};
-
-// ---------------------------------------------------------------- layer chains (chain.hip)
-// A run of consecutive low-resolution layers (depthwise 3x3 -> 1x1 BlazeBlocks and plain 1x1
-// convs, <= 256 positions and <= 128 channels per image) executed by ONE workgroup per image
-// with every activation in LDS: the chain reads its entry tensor from HBM once and writes only
-// the tensors consumed outside it (graph outputs, later layers).  LDS planes carry a one-cell
-// zero border ((H+2) x (W+2) per channel) so depthwise taps need no bounds checks.  The op table
-// is compiled into the session's weight buffer (all fields 32-bit, offsets in floats), so the
-// kernel reads it through the scalar cache; only binding-dependent pointers are arguments.
-enum ChainOpKind : int { CHAIN_DWPW = 0, CHAIN_PW = 1 };
-
-struct ChainAct {
-    int kind;
-    float lo, hi;
-    int slope_off;  // floats into the weight buffer, -1 when none
-};
-
-struct ChainOp {
-    int kind;
-    int in_off, res_off, out_off;   // LDS offsets (floats) of bordered planes; -1: none
-    int Cin, Cout, W, OP, OW;       // input channels / width; output positions / width
-    int in_ps, in_wp;               // input plane stride and bordered row width
-    int out_ps, out_wp;             // output plane stride and bordered row width
-    int res_ps, res_wp;             // residual source plane stride and bordered row width
-    int stride, pad_t, pad_l;       // depthwise geometry (CHAIN_DWPW)
-    int Mpad, MS, MTW, NTW, NT;     // 1x1 weights [Kpad16][Mpad]; consumer tiling (16x16 tiles)
-    int res_mode, r_C;
-    int w_off, b_off, dw_w_off, dw_b_off;
-    ChainAct pre, post, dw_act;
-    int gout;                       // global destination index (-1: none)
-    int ds;                         // depthwise-output row stride in the D buffers (floats)
-    int zero_border;                // the output region held another tensor: re-zero its border
-};
-static_assert(sizeof(ChainOp) % 4 == 0, "ChainOp is a table of 32-bit words");
-
-constexpr int CHAIN_MAX_OUTS = 8;
-// consumer tilings the kernel is instantiated for: {MTW, NTW} 16x16 tiles per consumer wave
-constexpr int CHAIN_CONSUMER_WAVES = 8;
-constexpr int CHAIN_TILINGS[][2] = {{1, 1}, {1, 2}, {1, 3}, {1, 9}, {2, 1}, {2, 2}, {3, 1}, {3, 2},
-                                    {3, 4}, {4, 1}, {4, 2}};
-
-struct ChainOut {  // element (n, c, q) at p + n*sN + c*sC + q*sP
-    float *p;
-    int64_t sN, sC, sP;
-};
-
-struct ChainParams {
-    const float *weights;
-    int ops_off, nops;              // op table at weights + ops_off (floats)
-    const float *entry;             // entry tensor, CNHW: (n, c, p) at entry + n*e_sN + c*e_sC + p
-    int64_t e_sN, e_sC;
-    int e_C, e_H, e_W, e_off;       // geometry and LDS offset (bordered planes)
-    int N;
-    int d_off, d_buf;               // D buffers: two of d_buf floats at LDS offset d_off
-    int p_off, p_buf;               // per-layer parameters staged in LDS: two of p_buf floats
-    int lds_floats;
-    ChainOut gout[CHAIN_MAX_OUTS];
-};
-
 // Kernel forms the launchers and the plan compiler choose between.  Every form computes the same
 // arithmetic in the same order, so switching one changes no output bit (tests/test_gpu_forms.py).
-// ZARU_HIP_FORMS, read once per process, switches forms off ("-dma,-v4") or the opt-in chain / ring
-// forms on ("+chain", "+ring"), for verification and A/B runs.
+// ZARU_HIP_FORMS, read once per process, switches forms off ("-dma,-v4"), for verification and
+// A/B runs.
 //   dma: LDS-DMA staged MFMA dwpw (dwpw_dma_kernel)   v4: windowed depthwise taps (dwpw_kernel)
 //   valu: VALU dwpw for few-channel high-resolution layers   valu_db: its double-buffered staging
-//   rows: image-row head GEMM (gemm_rows_kernel)   chain: low-resolution layer runs (chain.hip)
+//   rows: image-row head GEMM (gemm_rows_kernel)
 //   vres: VALU dwpw taking the block's residual from the staged depthwise taps
-//   vstore: 16-B row-segment GEMM epilogue   ring: persistent LDS-ring MFMA dwpw (dwpw_mfma.hip)
-//   ir: expand 1x1 + depthwise + project 1x1 (inverted residual) in one launch (ir.hip)
-enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_CHAIN, FORM_VRES, FORM_VSTORE, FORM_RING, FORM_IR, FORM_COUNT };
+//   vstore: 16-B row-segment GEMM epilogue
+enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_VRES, FORM_VSTORE, FORM_COUNT };
 bool form_on(Form f);
 
 bool stem_supported(int cin, int k, int stride, int cout);
@@ -278,7 +210,5 @@ const char *launch_candidates(const CandParams &p, hipStream_t s);
 const char *launch_stem(const StemParams &p, bool pre, hipStream_t s);
 const char *launch_dwpw(const DwPwParams &p, hipStream_t s);
 const char *launch_dwpw_mfma(const DwPwParams &p, hipStream_t s);  // the MFMA forms (dwpw_mfma.hip)
-const char *launch_ir(IrParams p, hipStream_t s);  // nullptr: the block does not fit the fused form
-const char *launch_chain(const ChainParams &p, hipStream_t s);
 
 }  // namespace zr

@@ -51,6 +51,7 @@ struct DetPostParams {
     int face;               // 1: angle = eye line vs +X (BlazeFace); 0: wrist -> MCP vs +Y (palm)
     int in_w, in_h;         // detector input
     float thresh, iou;
+    int mode;               // SuppressionMode: 0 Average (nms.rs:77-139), 1 Remove (nms.rs:70-76)
     int *count;             // [N] detections after NMS
     float *dets;            // [N][dcap][20] {conf, angle, cx, cy, w, h, 7 x (kx, ky)}, NMS order
     int dcap;
@@ -87,11 +88,12 @@ const char *launch_seed(const SeedParams &p, hipStream_t s);
 // 196-208), and decide whether this step's palm detection counts (210-218).
 struct HandManageParams {
     TrackState *state;       // [S * H] hand slots (the track update's output)
-    uint32_t *ids;           // [S * H]
+    uint64_t *ids;           // [S * H] HandId (tracking.rs:227, u64)
     float *hroi;             // [S * H][5] the hand's ROI (tracking.rs: TrackedHand::roi)
     int32_t *src;            // [S * H] out: slot of the hand before this call (-1: new hand)
     int32_t *nhands;         // [S]
-    uint32_t *next_id;       // [S]
+    uint64_t *next_id;       // [S]
+    int32_t *dropped;        // [S] out: kept palm detections this call found no free hand slot for
     double *next_det;        // [S] redetection clock (ms)
     int32_t *det_pending;    // [S] in: count/dets hold this stream's detections; out: this step's counts
     const int32_t *count;    // [S] detections (det_post)

@@ -76,10 +76,21 @@ class JpegDecoder:
         check(lib().zr_jpeg_decode_batch_async(self._h, n, bufs, lens, outs, strides, stream))
 
     def status(self):
-        """(device entropy decodes, host entropy decodes, corrupt flag) since creation."""
+        """(device entropy decodes, host entropy decodes since creation, corrupt flag of the last
+        call)."""
         g, h, c = C.c_uint64(), C.c_uint64(), C.c_int()
         check(lib().zr_jpeg_decoder_status(self._h, C.byref(g), C.byref(h), C.byref(c)))
         return g.value, h.value, c.value
+
+    def frame_errors(self):
+        """Per frame of the last call: True where its (device-decoded) entropy data was corrupt;
+        the rest of such an interval decodes as zero blocks (libjpeg-turbo's rule)."""
+        import numpy as np
+        n = C.c_size_t()
+        check(lib().zr_jpeg_frame_errors(self._h, None, 0, C.byref(n)))
+        flags = np.zeros(n.value, np.int32)
+        check(lib().zr_jpeg_frame_errors(self._h, flags.ctypes.data, n.value, C.byref(n)))
+        return flags.astype(bool)
 
     def decode(self, data: bytes):
         """Decode to a host numpy array [H, W, 4] (test / convenience path)."""
