@@ -67,9 +67,66 @@ def test_atan2f_random_pairs_match_glibc(gm):
     assert same.all(), np.nonzero(~same)[0][:10]
 
 
+VARIANT_CHILD = r"""
+import ctypes as C, json, sys
+import numpy as np
+out = {}
+for tag, path in (("fma", sys.argv[1]), ("nofma", sys.argv[2])):
+    L = C.CDLL(path)
+    for f in (L.gm_glibc, L.gm_mine):
+        f.restype = None
+        f.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+    L.gm_sweep.restype = C.c_uint64
+    L.gm_sweep.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64]
+    for fn, name in enumerate(("sinf", "cosf", "expf")):
+        a = np.array(json.load(open(sys.argv[3]))[name], np.uint32).view(np.float32)
+        g, m = np.empty_like(a), np.empty_like(a)
+        L.gm_glibc(fn, a.ctypes.data, None, g.ctypes.data, a.size)
+        L.gm_mine(fn, a.ctypes.data, None, m.ctypes.data, a.size)
+        out[f"{tag}/{name}"] = bool((g.view(np.uint32) == m.view(np.uint32)).all())
+        out[f"{tag}/{name}/sweep"] = int(L.gm_sweep(fn, 3, (1 << 32) // 4093, 4093))
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("tunables", ["", "glibc.cpu.hwcaps=-AVX2,-FMA"])
+def test_both_glibc_builds_are_restated(tunables):
+    """glibc picks sinf / cosf / expf per CPU through IFUNCs: the -mfma builds on FMA hosts (this
+    image, the GPU box), the baseline builds otherwise; they round differently on 36 of the 3 x 2^32
+    inputs (tests/golden/glibc_fma_variant_inputs.json, tools/libm_variants.cpp).  With the
+    baseline build forced (GLIBC_TUNABLES=glibc.cpu.hwcaps=-AVX2,-FMA) glibc must agree with the
+    ZR_GLIBC_FMA=0 restatement on those inputs and disagree with the FMA one, and by default the
+    reverse; a strided sweep must agree everywhere else.  profiles/r04_libm_exhaustive_nofma.json
+    holds the all-inputs run of the baseline build under the same tunable."""
+    import subprocess
+    import sys
+    nofma = os.path.join(REPO, "tests", "native", "libglibc_math_check_nofma.so")
+    if not os.path.exists(nofma):
+        pytest.fail(f"{nofma} missing: run __graft_entry__.build()")
+    env = dict(os.environ)
+    if tunables:
+        env["GLIBC_TUNABLES"] = tunables
+    r = subprocess.run([sys.executable, "-c", VARIANT_CHILD, LIB, nofma,
+                        os.path.join(REPO, "tests", "golden", "glibc_fma_variant_inputs.json")],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout)
+    resolved = "nofma" if tunables else "fma"
+    other = "fma" if tunables else "nofma"
+    for name in ("sinf", "cosf", "expf"):
+        assert res[f"{resolved}/{name}"], (tunables, name)
+        assert not res[f"{other}/{name}"], (tunables, name)
+        assert res[f"{resolved}/{name}/sweep"] == 0, (tunables, name)
+
+
 def test_exhaustive_record_is_clean():
     """profiles/r03_libm_exhaustive.json: tools/libm_exhaustive.cpp over all 2^32 inputs."""
     rec = json.load(open(os.path.join(REPO, "profiles", "r03_libm_exhaustive.json")))
     assert rec["inputs_each"] == 1 << 32 and rec["atan2f_pairs"] == 1 << 32
+    for k in ("sinf", "cosf", "expf", "atanf", "atan2f"):
+        assert rec[f"{k}_mismatch"] == 0, k
+    # the baseline (ZR_GLIBC_FMA=0) build against glibc forced to its baseline IFUNCs
+    rec = json.load(open(os.path.join(REPO, "profiles", "r04_libm_exhaustive_nofma.json")))
+    assert rec["fma_build"] == 0 and rec["inputs_each"] == 1 << 32 and rec["atan2f_pairs"] >= 1 << 30
     for k in ("sinf", "cosf", "expf", "atanf", "atan2f"):
         assert rec[f"{k}_mismatch"] == 0, k

@@ -9,8 +9,8 @@ post-processing options of Detector (crates/zaru/src/detection.rs:44-111,186-202
 * the default detection capacity keeps every NMS output (the reference's Detections is a Vec),
   and a smaller cap reports what it drops.
 
-Palm detections on noise frames need a low threshold (Detector::set_threshold): 0.2 gives dozens
-per frame, which exercises grouping, ordering and capacity."""
+Palm detections on noise frames need a low threshold (Detector::set_threshold): at 0.05 the oracle
+puts 33-76 anchors of such frames above it, which exercises grouping, ordering and capacity."""
 import numpy as np
 import pytest
 
@@ -46,7 +46,7 @@ def _dets(p):
             for ds in p.detections()]
 
 
-@pytest.mark.parametrize("kind,thresh", [("face", 0.5), ("hand", 0.2)])
+@pytest.mark.parametrize("kind,thresh", [("face", 0.5), ("hand", 0.05)])
 def test_device_records_equal_host_packed(frames, kind, thresh):
     import zaru_amd.host as H_
     _, flist, forced = frames
@@ -89,14 +89,14 @@ def test_nms_remove_device_equals_host(frames):
     empty = [[] for _ in range(NF)]
     got = []
     for device_post in (True, False):
-        p = _pipe(H_, "hand", nms_mode="remove", det_threshold=0.2, device_post=device_post)
+        p = _pipe(H_, "hand", nms_mode="remove", det_threshold=0.05, device_post=device_post)
         p.set_frames(flist, empty)
         p.run_frames()
         got.append(_dets(p))
     assert got[0] == got[1]
     assert sum(len(d) for d in got[0]) >= NF
     # Remove keeps seeds as decoded, Average merges groups: the two modes really differ here
-    p = _pipe(H_, "hand", det_threshold=0.2)
+    p = _pipe(H_, "hand", det_threshold=0.05)
     p.set_frames(flist, empty)
     p.run_frames()
     assert _dets(p) != got[0]
@@ -106,17 +106,17 @@ def test_detection_capacity(frames):
     import zaru_amd.host as H_
     _, flist, _ = frames
     empty = [[] for _ in range(NF)]
-    full = _pipe(H_, "hand", det_threshold=0.2)  # default capacity: the 2016 anchors
+    full = _pipe(H_, "hand", det_threshold=0.05)  # default capacity: the 2016 anchors
     full.set_frames(flist, empty)
     full.run_frames()
     counts = [len(d) for d in full.detections()]
     assert full.times()["dropped_detections"] == 0
     assert max(counts) > 4, counts  # more than any small cap: the default keeps them all
-    host = _pipe(H_, "hand", det_threshold=0.2, device_post=False)
+    host = _pipe(H_, "hand", det_threshold=0.05, device_post=False)
     host.set_frames(flist, empty)
     host.run_frames()
     assert _dets(full) == _dets(host)
-    capped = _pipe(H_, "hand", det_threshold=0.2, det_cap=4)
+    capped = _pipe(H_, "hand", det_threshold=0.05, det_cap=4)
     capped.set_frames(flist, empty)
     capped.run_frames()
     assert capped.times()["dropped_detections"] == sum(max(0, c - 4) for c in counts)

@@ -21,6 +21,14 @@ struct zr_comm {
 
 namespace {
 
+// RCCL's own HIP calls (capture queries on the caller's stream among them) may leave the thread's
+// last-error slot set although the call succeeded; the runtime's next hipGetLastError() check after
+// a kernel launch would then report RCCL's stale status as its own failure.  Every entry point
+// here clears it before returning.
+struct ClearLastError {
+    ~ClearLastError() { (void)hipGetLastError(); }
+};
+
 int nccl_err(const char *what, ncclResult_t r) {
     return zr_internal::set_error(ZR_ERR_DEVICE, std::string(what) + ": " + ncclGetErrorString(r));
 }
@@ -41,6 +49,7 @@ int guarded(F &&body) noexcept {
 extern "C" {
 
 int zr_comm_unique_id(uint8_t id[128]) {
+    ClearLastError clear;
     return guarded([&]() -> int {
         static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
         if (!id) return zr_internal::set_error(ZR_ERR_INVALID_ARGUMENT, "null id");
@@ -52,6 +61,7 @@ int zr_comm_unique_id(uint8_t id[128]) {
 }
 
 int zr_comm_create(const uint8_t id[128], int nranks, int rank, int device, zr_comm **out) {
+    ClearLastError clear;
     return guarded([&]() -> int {
         if (!id || !out || nranks <= 0 || rank < 0 || rank >= nranks)
             return zr_internal::set_error(ZR_ERR_INVALID_ARGUMENT, "bad communicator arguments");
@@ -74,12 +84,14 @@ int zr_comm_create(const uint8_t id[128], int nranks, int rank, int device, zr_c
 }
 
 void zr_comm_destroy(zr_comm *c) {
+    ClearLastError clear;
     if (!c) return;
     if (c->comm) (void)ncclCommDestroy(c->comm);
     delete c;
 }
 
 int zr_comm_all_gather_async(zr_comm *c, const void *d_send, void *d_recv, size_t bytes, void *hip_stream) {
+    ClearLastError clear;
     return guarded([&]() -> int {
         if (!c || !c->comm || !d_send || !d_recv)
             return zr_internal::set_error(ZR_ERR_INVALID_ARGUMENT, "null communicator or buffer");
