@@ -105,6 +105,9 @@ def parse():
     ap.add_argument("--host-post", action="store_true",
                     help="decode/NMS/map and the tracker update on host threads (the host restatement) "
                          "instead of on the device")
+    ap.add_argument("--self-gather", action="store_true",
+                    help="N = 1 only: run the N > 1 data path (device records + an RCCL all-gather per step "
+                         "over a one-rank communicator), to price it on one GPU")
     ap.add_argument("--prime-seconds", type=float, default=0.6,
                     help="untimed pipeline priming before the warmup steps (see prime())")
     return ap.parse_args()
@@ -469,6 +472,9 @@ def main():
                 comms.append(Comm(bytes(uid.numpy().tobytes()), world, rank, device))
         else:
             gather = shard.RecordGather(args.batch * len(wls), shard.record_width(), "cpu")
+    if world == 1 and args.self_gather:  # the N > 1 data path on one GPU: a one-rank communicator
+        comms = [Comm(Comm.unique_id(), 1, 0, device) for _ in wls]
+    if world > 1 or comms:
         # global frame ids: rank + world * i, the second workload's after the first's
         for j, w in enumerate(wls):
             w.pipe.enable_records(shard.REC_DETS, rank + j * world * w.batch, world,
@@ -553,7 +559,9 @@ def main():
                    + ((", device-written detection records copied to the host and all-gathered over gloo "
                        "each step (shared-GPU dry run: gloo has no device path)" if share
                        else ", one RCCL all-gather per step of the detection records the post-processing "
-                       "kernel writes on the device, on the pipeline's gather stream") if world > 1 else "")},
+                       "kernel writes on the device, on the pipeline's gather stream") if world > 1
+                      else (", with the N > 1 data path (device records + an RCCL all-gather per step over a "
+                            "one-rank communicator)" if comms else ""))},
         "prime": primed,
         "gather_check": gather_check,
         "frames_per_s": round(frames / elapsed, 1),

@@ -2,7 +2,8 @@
 so switching a form (ZARU_HIP_FORMS, read once per process) must not change one bit of any model
 output.  Each configuration runs in a child process (the switches are process-wide); the
 batch is large enough that every form the default build picks is exercised (LDS-DMA staged
-VALU and MFMA forms, the windowed V4 taps, the image-row head GEMM).
+VALU and MFMA forms, the windowed V4 taps, the image-row head GEMM); the warp-specialized MFMA
+form has a test of its own at 1024 hand ROIs.
 """
 import os
 import subprocess
@@ -40,7 +41,8 @@ SWITCHES = {
     "no_rows": "-rows",
     "no_vres": "-vres",
     "no_vstore": "-vstore",
-    "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore",
+    "no_ws": "-ws",
+    "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws",
 }
 
 
@@ -95,3 +97,39 @@ def test_nonsquare_full_plane_conv(forms):
     r = subprocess.run([sys.executable, "-c", NONSQUARE_CHILD, REPO], env=e, capture_output=True, text=True,
                        timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+# The warp-specialized form runs only on launches with about a tile per CU or more (the hand
+# network's 14^2 / 7^2 blocks from ~940 ROIs): a batch of its own, with the launched kernels read
+# back from the session profile so the test knows the form ran.
+WS_CHILD = r"""
+import sys, ctypes as C, numpy as np
+sys.path.insert(0, sys.argv[1])
+from zaru_amd.nn import NeuralNetwork, model_bytes
+from zaru_amd._lib import lib, check
+net = NeuralNetwork.from_onnx(model_bytes("hand_landmark_lite")).load()
+check(lib().zr_profile_enable(net._h, 1))
+x = np.random.default_rng(9).uniform(-1.0, 1.0, size=(1024, 3, 224, 224)).astype(np.float32)
+outs = net.estimate(x)
+need = C.c_size_t()
+buf = C.create_string_buffer(1 << 20)  # (a read returns and clears the aggregate: one call)
+check(lib().zr_profile_read(net._h, buf, len(buf), C.byref(need)))
+kernels = np.array([l.split()[0] for l in buf.value.decode().splitlines() if l.strip()])
+np.savez(sys.argv[2], kernels=kernels, **{f"o{i}": o for i, o in enumerate(outs)})
+"""
+
+
+def test_ws_form_is_bitwise_neutral(tmp_path):
+    res = {}
+    for name, env in (("default", ""), ("no_ws", "-ws")):
+        path = str(tmp_path / f"{name}.npz")
+        subprocess.run([sys.executable, "-c", WS_CHILD, REPO, path], env=dict(os.environ, ZARU_HIP_FORMS=env),
+                       check=True, timeout=110)
+        with np.load(path) as z:
+            res[name] = {k: z[k] for k in z.files}
+    ws = [k for k in res["default"]["kernels"] if k.startswith("dwpw_ws_kernel")]
+    assert len(ws) == 4, res["default"]["kernels"]  # 3x3 14^2, 5x5 14^2, 5x5/2 14->7, 5x5 7^2
+    assert not any(k.startswith("dwpw_ws_kernel") for k in res["no_ws"]["kernels"])
+    for k in res["default"]:
+        if k != "kernels":
+            assert np.array_equal(res["default"][k], res["no_ws"][k]), (k, float(np.abs(res["default"][k] - res["no_ws"][k]).max()))

@@ -17,6 +17,7 @@ for s in ${STEPS//,/ }; do
     hand) timeout -k 10 300 python bench.py --workload hand --batch 256 --steps 30 --warmup 5 --no-cpu-baseline --no-traffic "$@" > $O/hand.json 2> $O/hand.err ;;
     both) timeout -k 10 300 python bench.py --workload both --steps 30 --warmup 5 --no-cpu-baseline --no-traffic --no-profile "$@" > $O/both.json 2> $O/both.err ;;
     n1) timeout -k 10 300 python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-traffic --no-profile $NOSIDE "$@" > $O/n1.json 2> $O/n1.err ;;
+    n1g) timeout -k 10 300 python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-traffic --no-profile --self-gather $NOSIDE "$@" > $O/n1g.json 2> $O/n1g.err ;;
     n2) ZARU_BENCH_SHARE_GPU=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
           --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 50 --warmup 10 --no-cpu-baseline \
           --no-traffic --no-profile $NOSIDE "$@" > $O/n2.json 2> $O/n2.err ;;

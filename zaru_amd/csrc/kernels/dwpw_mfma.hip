@@ -531,6 +531,7 @@ const char *dwpw_layout(const DwPwParams &p, const DwPwLayout &l, hipStream_t s)
 // among those, the widest column tile that still gives >= 4 workgroups per CU (else the most
 // workgroups).
 const char *launch_dwpw_mfma(const DwPwParams &p, hipStream_t s) {
+    if (const char *k = launch_dwpw_ws(p, s)) return k;
     // workgroups one launch should reach (ZARU_HIP_MINWGS overrides it for layout sweeps)
     static const int64_t min_wgs = [] {
         const char *e = std::getenv("ZARU_HIP_MINWGS");

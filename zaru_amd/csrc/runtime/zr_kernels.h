@@ -187,7 +187,8 @@ struct DwPwParams {
 //   rows: image-row head GEMM (gemm_rows_kernel)
 //   vres: VALU dwpw taking the block's residual from the staged depthwise taps
 //   vstore: 16-B row-segment GEMM epilogue
-enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_VRES, FORM_VSTORE, FORM_COUNT };
+//   ws: warp-specialized persistent MFMA dwpw (dwpw_ws.hip)
+enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_VRES, FORM_VSTORE, FORM_WS, FORM_COUNT };
 bool form_on(Form f);
 
 bool stem_supported(int cin, int k, int stride, int cout);
@@ -210,5 +211,6 @@ const char *launch_candidates(const CandParams &p, hipStream_t s);
 const char *launch_stem(const StemParams &p, bool pre, hipStream_t s);
 const char *launch_dwpw(const DwPwParams &p, hipStream_t s);
 const char *launch_dwpw_mfma(const DwPwParams &p, hipStream_t s);  // the MFMA forms (dwpw_mfma.hip)
+const char *launch_dwpw_ws(const DwPwParams &p, hipStream_t s);    // nullptr: the layer does not fit it
 
 }  // namespace zr
