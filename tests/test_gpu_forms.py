@@ -42,7 +42,9 @@ SWITCHES = {
     "no_vres": "-vres",
     "no_vstore": "-vstore",
     "no_ws": "-ws",
-    "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws",
+    "no_groups": "-groups",
+    "no_dwgap": "-dwgap",
+    "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws,-groups,-dwgap",
 }
 
 

@@ -169,8 +169,9 @@ def test_truncated_scan_is_decoded_or_rejected(dec):
 
 def test_restart_streams_decode_on_the_device(dec):
     """Streams with >= 8 restart intervals short enough for a workgroup's LDS are entropy-decoded
-    on the GPU (decoder status), with no corrupt interval flagged; streams without DRI, and ones
-    whose intervals are too long, stay on the host path."""
+    on the GPU (decoder status), with no corrupt interval flagged; so are streams without DRI
+    (self-synchronising decoder, jpeg_sync.hip); restart streams whose intervals are too long stay
+    on the host path."""
     from zaru_amd.jpeg import JpegDecoder
     d = JpegDecoder(0)
     try:
@@ -182,7 +183,7 @@ def test_restart_streams_decode_on_the_device(dec):
         for data in (with_rst, long_rst, plain, gray_rst):
             assert np.array_equal(d.decode(data), libjpeg_turbo_rgba(data))
         gpu, host, corrupt = d.status()
-        assert (gpu, host, corrupt) == (2, 2, 0)
+        assert (gpu, host, corrupt) == (3, 1, 0)
     finally:
         d.close()
 
@@ -296,8 +297,8 @@ def test_restart_stream_cut_mid_scan(dec):
 
 def test_batch_decode_mixed_frames(dec):
     """zr_jpeg_decode_batch_async: frames of different sizes, subsamplings and entropy paths
-    (restart intervals -> one shared device Huffman launch; no DRI / long intervals -> host) in
-    one call, each equal to libjpeg-turbo's decode."""
+    (restart intervals -> one shared device Huffman launch; no DRI -> the self-synchronising
+    device decoder; long intervals -> host) in one call, each equal to libjpeg-turbo's decode."""
     from zaru_amd._lib import DeviceBuffer, lib
     from zaru_amd.jpeg import JpegDecoder
     specs = [((1080, 1920), 90, 2, {"restart_marker_blocks": 4}),
@@ -317,7 +318,7 @@ def test_batch_decode_mixed_frames(dec):
         lib().zr_stream_synchronize(None)
         for i, (data, (h, w)) in enumerate(zip(datas, shapes)):
             assert np.array_equal(bufs[i].download((h, w, 4), "uint8"), libjpeg_turbo_rgba(data)), i
-        assert d.status() == (4, 3, 0)
+        assert d.status() == (6, 1, 0)
     finally:
         d.close()
 

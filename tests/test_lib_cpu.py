@@ -26,12 +26,12 @@ def test_library_exports_header_symbols():
     assert {s for s, _, _ in _lib.SIGNATURES} == set(syms)
 
 
-KINDS = ("gemm", "dw", "direct", "elt", "resize", "gap", "dwpw")
+KINDS = ("gemm", "dw", "direct", "elt", "resize", "gap", "dwpw", "dwgap")
 
 
 @pytest.mark.parametrize("model,launches", [
     ("face_detection_short_range", 21), ("face_landmark", 25),
-    ("palm_detection_lite", 32), ("hand_landmark_lite", 37)])
+    ("palm_detection_lite", 32), ("hand_landmark_lite", 36)])
 def test_plan_compiles_and_fuses(models_dir, model, launches):
     path = os.path.join(models_dir, model + ".onnx")
     txt = _lib.plan_describe(open(path, "rb").read())
@@ -197,3 +197,48 @@ def test_plan_reads_only_produced_tensors(models_dir, model):
             t = r.split("[")[0]
             assert t == "in0" or t in produced, (model, line)
         produced.add(re.search(r" out=(\S+)", line).group(1).split("[")[0])
+
+
+def _steps(txt):
+    return [l for l in txt.splitlines() if l.split(" ")[0] in KINDS]
+
+
+def _field(line, key):
+    return re.search(rf"\b{key}=(\S+)", line).group(1)
+
+
+def _tname(ref):
+    return ref.split("[")[0]
+
+
+def test_sibling_steps_share_launches(models_dir):
+    """the FaceMesh flag and mesh branches after the 6^2 trunk (t28) run as
+    shared launches, layer by layer, and the hand network's four heads as one; a group's members
+    never read each other's outputs."""
+    fm = _steps(_lib.plan_describe(open(os.path.join(models_dir, "face_landmark.onnx"), "rb").read()))
+    first = next(i for i, l in enumerate(fm) if _field(l, "in").startswith("t28["))
+    tail = fm[first:]
+    launches = [l for l in tail if _field(l, "grp") != "0"]
+    assert len(launches) <= 6, "\n".join(tail)
+    heads = [l for l in tail if _field(l, "out").startswith("out")]
+    assert [_field(l, "grp") for l in heads] == ["2", "0"]
+    hand = _steps(_lib.plan_describe(open(os.path.join(models_dir, "hand_landmark_lite.onnx"), "rb").read()))
+    hheads = [l for l in hand if _field(l, "out").startswith("out")]
+    assert [_field(l, "grp") for l in hheads] == ["4", "0", "0", "0"]
+    for steps in (fm, hand):
+        for i, l in enumerate(steps):
+            g = int(_field(l, "grp"))
+            members = steps[i:i + g] if g >= 2 else []
+            outs = {_tname(_field(m, "out")) for m in members}
+            for m in members:
+                assert _tname(_field(m, "in")) not in outs
+                assert _tname(_field(m, "in2")) not in outs
+
+
+def test_groups_switch_off(models_dir):
+    code = ("import sys; sys.path.insert(0, sys.argv[1]); from zaru_amd import _lib; "
+            "print(_lib.plan_describe(open(sys.argv[2], 'rb').read()))")
+    r = subprocess.run([sys.executable, "-c", code, REPO, os.path.join(models_dir, "face_landmark.onnx")],
+                       env=dict(os.environ, ZARU_HIP_FORMS="-groups"), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert all(_field(l, "grp") == "1" for l in _steps(r.stdout))

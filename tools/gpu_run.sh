@@ -24,6 +24,8 @@ for s in ${STEPS//,/ }; do
     n2half) ZARU_BENCH_SHARE_GPU=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
           --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 2 --batch 512 --steps 50 --warmup 10 \
           --no-cpu-baseline --no-traffic --no-profile $NOSIDE "$@" > $O/n2half.json 2> $O/n2half.err ;;
+    jpeg) timeout -k 10 400 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-traffic --no-profile \
+          --no-hand --no-next --no-tracking --no-c5 "$@" > $O/jpeg.json 2> $O/jpeg.err ;;
     prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py \
           --steps 20 --warmup 5 --no-cpu-baseline --no-traffic $NOSIDE "$@" > $O/bench_prof.json 2> $O/prof.err ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -11,6 +11,7 @@
 #include "../runtime/zr_kernels.h"
 #include "act.h"
 #include "epilogue.h"
+#include "group.h"
 #include "lds_dma.h"
 
 namespace zr {
@@ -257,8 +258,7 @@ __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) 
 // those layouts stage the weights' chunk rows in the DMA buffer.
 // (MTW == 1: 4 waves per SIMD fit in 128 registers without spills)
 template <int K, int S, int WM, int MTW, int DFKC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTW == 1 ? 4 : 1)))
-void dwpw_dma_kernel(const DwPwParams P, int nct, int runmax, int bufsz) {
+__device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int runmax, int bufsz, int bx, int by, int gx) {
     constexpr int WN = 4 / WM, BN = WN * 32, BM = WM * MTW * 32, KK = K * K;
     constexpr int CPAR = 256 / BN, PER = DFKC / CPAR;
     constexpr int KKP = (DFKC * KK + 3) / 4 * 4;
@@ -270,13 +270,13 @@ void dwpw_dma_kernel(const DwPwParams P, int nct, int runmax, int bufsz) {
     float *sD = smem + 2 * bufsz;
     const GemmParams &G = P.g;
 
-    const int cpx = gridDim.x >> 3;  // gridDim.x is a multiple of 8
-    const int tile = (blockIdx.x & 7) * cpx + (blockIdx.x >> 3);
+    const int cpx = gx >> 3;  // the grid's x extent is a multiple of 8
+    const int tile = (bx & 7) * cpx + (bx >> 3);
     if (tile >= nct) return;  // whole workgroup, before any barrier
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int kh = lane >> 5, col = lane & 31;
     const int wm = wave % WM, wn = wave / WM;
-    const int j0 = tile * BN, m0 = blockIdx.y * BM;
+    const int j0 = tile * BN, m0 = by * BM;
     const int Cin = G.K, H = P.in.H, W = P.in.W, Pin = H * W, OW = P.OW, Pq = G.P;
     const int pt = P.pad_t, pl = P.pad_l;
 
@@ -422,6 +422,20 @@ void dwpw_dma_kernel(const DwPwParams P, int nct, int runmax, int bufsz) {
     for (int t = 0; t < MTW; ++t) epilogue_tile(G, acc[t], on, oq, m0 + (wm * MTW + t) * 32, kh);
 }
 
+template <int K, int S, int WM, int MTW, int DFKC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTW == 1 ? 4 : 1)))
+void dwpw_dma_kernel(const DwPwParams P, int nct, int runmax, int bufsz) {
+    dwpw_dma_body<K, S, WM, MTW, DFKC>(P, nct, runmax, bufsz, blockIdx.x, blockIdx.y, gridDim.x);
+}
+
+// sibling layers in one launch (group.h): a0 = nct, a1 = runmax, a2 = bufsz of each part
+template <int K, int S, int WM, int MTW, int DFKC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTW == 1 ? 4 : 1)))
+void dwpw_dma_group_kernel(const LaunchGroup<DwPwParams> G) {
+    const GroupSlot t = group_slot(G);
+    dwpw_dma_body<K, S, WM, MTW, DFKC>(G.p[t.g], G.a0[t.g], G.a1[t.g], G.a2[t.g], t.bx, t.by, G.gx[t.g]);
+}
+
 namespace {
 
 struct DwPwLayout {
@@ -470,13 +484,22 @@ static size_t dma_plan(const DwPwParams &p, int *runmax, int *bufsz) {
 }
 
 // the widest channel chunk the DMA form may use (ZARU_HIP_DFKC: 16 / 32 / 64, for A/B runs)
-static int dfkc_max() {
+static int dfkc_env() {
     static const int v = [] {
         const char *e = std::getenv("ZARU_HIP_DFKC");
         const long x = e ? std::strtol(e, nullptr, 10) : 0;
-        return x >= 64 ? 64 : x >= 32 ? 32 : 16;
+        return x >= 64 ? 64 : x >= 32 ? 32 : x > 0 ? 16 : 0;
     }();
     return v;
+}
+
+// Channel chunk of the 3x3 MTW = 1 layouts: 32 for launches of < 512 workgroups (FaceMesh's
+// 6^2 / 3^2 blocks at 341 images: half the dependent DMA round trips of a workgroup that is
+// alone on its CU, 18.9 -> 17.0 us at 3^2, profiles/r04_layers/), else 16 (at 12^2 and up the
+// wider chunk's DMA costs more than the barriers it saves: r03).  ZARU_HIP_DFKC forces one.
+static int dfkc_for(int wgs) {
+    if (const int e = dfkc_env()) return e;
+    return wgs < 512 ? 32 : 16;
 }
 
 template <int K, int S, int WM, int MTW>
@@ -489,12 +512,13 @@ const char *dwpw_go(const DwPwParams &p, hipStream_t s) {
     if constexpr (K == 3 && MTW == 1) {
         // wider channel chunks: fewer dependent DMA round trips per tile (the 6^2 / 3^2 launches
         // of a few dozen workgroups are nothing but those round trips)
-        if (dfkc_max() >= 64)
+        const int dk = dfkc_for(nct * mb);
+        if (dk >= 64)
             if (const size_t lds = dma_plan<K, S, WM, MTW, 64>(p, &runmax, &bufsz)) {
                 hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, 64>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
                 return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,64>", K, S, WM, MTW);
             }
-        if (dfkc_max() >= 32)
+        if (dk >= 32)
             if (const size_t lds = dma_plan<K, S, WM, MTW, 32>(p, &runmax, &bufsz)) {
                 hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, 32>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
                 return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,32>", K, S, WM, MTW);
@@ -530,8 +554,7 @@ const char *dwpw_layout(const DwPwParams &p, const DwPwLayout &l, hipStream_t s)
 // Layout choice for the MFMA forms: no M split unless Mpad > 256, at most 1/3 padded rows;
 // among those, the widest column tile that still gives >= 4 workgroups per CU (else the most
 // workgroups).
-const char *launch_dwpw_mfma(const DwPwParams &p, hipStream_t s) {
-    if (const char *k = launch_dwpw_ws(p, s)) return k;
+static const DwPwLayout *choose_layout(const DwPwParams &p) {
     // workgroups one launch should reach (ZARU_HIP_MINWGS overrides it for layout sweeps)
     static const int64_t min_wgs = [] {
         const char *e = std::getenv("ZARU_HIP_MINWGS");
@@ -570,8 +593,75 @@ const char *launch_dwpw_mfma(const DwPwParams &p, hipStream_t s) {
             }
         }
     }
+    return best;
+}
+
+const char *launch_dwpw_mfma(const DwPwParams &p, hipStream_t s) {
+    if (const char *k = launch_dwpw_ws(p, s, true)) return k;
+    const DwPwLayout *best = choose_layout(p);
     if (p.k == 3) return p.stride == 1 ? dwpw_layout<3, 1>(p, *best, s) : dwpw_layout<3, 2>(p, *best, s);
     return p.stride == 1 ? dwpw_layout<5, 1>(p, *best, s) : dwpw_layout<5, 2>(p, *best, s);
+}
+
+namespace {
+
+template <int K, int S, int WM, int MTW, int DFKC>
+const char *dma_group(const DwPwParams *p, int n, hipStream_t s) {
+    constexpr int BN = (4 / WM) * 32, BM = WM * MTW * 32;
+    LaunchGroup<DwPwParams> G{};
+    G.n = n;
+    size_t lds = 0;
+    int total = 0;
+    for (int i = 0; i < n; ++i) {
+        int runmax = 0, bufsz = 0;
+        const size_t l = dma_plan<K, S, WM, MTW, DFKC>(p[i], &runmax, &bufsz);
+        if (!l) return nullptr;
+        lds = std::max(lds, l);
+        const int nct = (p[i].g.ncols + BN - 1) / BN, mb = (p[i].g.Mpad + BM - 1) / BM;
+        G.p[i] = p[i];
+        G.a0[i] = nct, G.a1[i] = runmax, G.a2[i] = bufsz;
+        G.gx[i] = (nct + 7) / 8 * 8;
+        G.start[i] = total;
+        total += G.gx[i] * mb;
+    }
+    for (int i = n; i <= ZR_GROUP_MAX; ++i) G.start[i] = total;
+    hipLaunchKernelGGL((dwpw_dma_group_kernel<K, S, WM, MTW, DFKC>), dim3(total), dim3(256), lds, s, G);
+    return kernel_name("dwpw_dma_group_kernel<%d,%d,%d,%d,%d>", K, S, WM, MTW, DFKC);
+}
+
+template <int K, int S, int DFKC>
+const char *dma_group_layout(const DwPwParams *p, int n, const DwPwLayout &l, hipStream_t s) {
+    switch (l.wm * 10 + l.mtw) {  // the layouts of the 6^2 / 3^2 sibling blocks (FaceMesh heads)
+    case 11: return dma_group<K, S, 1, 1, DFKC>(p, n, s);
+    case 21: return dma_group<K, S, 2, 1, DFKC>(p, n, s);
+    case 41: return dma_group<K, S, 4, 1, DFKC>(p, n, s);
+    default: return nullptr;
+    }
+}
+
+}  // namespace
+
+// Sibling MFMA dwpw layers in one launch when every part takes the LDS-DMA form with the same
+// kernel, layout and 16-channel chunks; nullptr otherwise (the caller launches them one by one).
+const char *launch_dwpw_mfma_group(const DwPwParams *p, int n, hipStream_t s) {
+    if (n < 2 || n > ZR_GROUP_MAX) return nullptr;
+    const DwPwLayout *l0 = nullptr;
+    for (int i = 0; i < n; ++i) {
+        if (p[i].k != p[0].k || p[i].stride != p[0].stride || launch_dwpw_ws(p[i], s, false)) return nullptr;
+        const DwPwLayout *l = choose_layout(p[i]);
+        if (l0 && (l->wm != l0->wm || l->mtw != l0->mtw)) return nullptr;
+        l0 = l;
+    }
+    if (p[0].k != 3 || l0->mtw != 1) return nullptr;
+    // the chunk each part would use alone (the rule on the whole group's workgroups: at most
+    // twice one part's, so the group keeps the parts' chunk unless that crosses the threshold)
+    const int bn = (4 / l0->wm) * 32;
+    int wgs = 0;
+    for (int i = 0; i < n; ++i) wgs = std::max(wgs, (p[i].g.ncols + bn - 1) / bn);
+    const int dk = dfkc_for(wgs);
+    if (dk == 32) return p[0].stride == 1 ? dma_group_layout<3, 1, 32>(p, n, *l0, s) : dma_group_layout<3, 2, 32>(p, n, *l0, s);
+    if (dk == 16) return p[0].stride == 1 ? dma_group_layout<3, 1, 16>(p, n, *l0, s) : dma_group_layout<3, 2, 16>(p, n, *l0, s);
+    return nullptr;
 }
 
 

@@ -343,7 +343,7 @@ __global__ __launch_bounds__(512) void dwpw_ws_kernel(const DwPwParams P, const 
 }
 
 template <int K, int S, int R, int WM, int MTW, int NTW>
-const char *ws_go(const DwPwParams &p, hipStream_t s) {
+const char *ws_go(const DwPwParams &p, hipStream_t s, bool launch) {
     constexpr int FC = WS_FC, BN = (4 / WM) * NTW * 32, KKP = (FC * K * K + 3) / 4 * 4;
     constexpr int PL = DwPad<K, S>::L;
     const GemmParams &g = p.g;
@@ -382,6 +382,7 @@ const char *ws_go(const DwPwParams &p, hipStream_t s) {
     const size_t lds = sizeof(float) * (size_t)(L.o_d + 2 * FC * BN);
     const int G = (std::min(L.nct, ncu) + 7) / 8 * 8;
     L.tpx = (L.nct + 7) / 8;
+    if (!launch) return "dwpw_ws_kernel";
     static const bool attr = hipFuncSetAttribute((const void *)dwpw_ws_kernel<K, S, R, WM, MTW, NTW>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
     (void)attr;
@@ -396,10 +397,10 @@ bool ws_enabled() { return form_on(FORM_WS); }  // ZARU_HIP_FORMS=-ws: the per-t
 // their depthwise LDS reads (profiles/r04_layers/).  The lower-resolution face / palm layers keep
 // the per-tile forms: a persistent kernel of BN-column tiles leaves most CUs idle there.
 // Mpad <= 64 -> 2 x 2 waves, <= 128 -> 4 x 1; N tiles per wave so a tile holds whole rows.
-#define ZR_WS64(K, S, R, NT) if (mp <= 64) return ws_go<K, S, R, 2, 1, NT>(p, s);
-#define ZR_WS128(K, S, R, NT) if (mp <= 128) return ws_go<K, S, R, 4, 1, NT>(p, s);
+#define ZR_WS64(K, S, R, NT) if (mp <= 64) return ws_go<K, S, R, 2, 1, NT>(p, s, launch);
+#define ZR_WS128(K, S, R, NT) if (mp <= 128) return ws_go<K, S, R, 4, 1, NT>(p, s, launch);
 
-const char *ws_dispatch(const DwPwParams &p, hipStream_t s) {
+const char *ws_dispatch(const DwPwParams &p, hipStream_t s, bool launch) {
     const int mp = p.g.Mpad, ow = p.OW;
     if (p.k == 3 && p.stride == 1 && ow == 14) { ZR_WS64(3, 1, 14, 7) }
     if (p.k == 5 && p.stride == 1 && ow == 14) { ZR_WS64(5, 1, 14, 7) }
@@ -413,13 +414,14 @@ const char *ws_dispatch(const DwPwParams &p, hipStream_t s) {
 }  // namespace
 
 // nullptr when the layer does not fit the form: an input that is not a plain CNHW tensor with
-// 16-B aligned channel planes, or a (kernel, stride, width, Mpad) without an instance above
-const char *launch_dwpw_ws(const DwPwParams &p, hipStream_t s) {
+// 16-B aligned channel planes, or a (kernel, stride, width, Mpad) without an instance above, or
+// too few tiles.  launch = false: only whether it would run.
+const char *launch_dwpw_ws(const DwPwParams &p, hipStream_t s, bool launch) {
     if (!ws_enabled() || p.g.K % 4 || p.in.sN != (int64_t)p.in.H * p.in.W || p.in.sC % 4 ||
         ((uintptr_t)p.in.p | (uintptr_t)p.g.wt | (uintptr_t)p.dw_w | (uintptr_t)p.dw_b) % 16 ||
         (p.dw_act.kind == ACT_PRELU && (uintptr_t)p.dw_act.slope % 16))
         return nullptr;
-    return ws_dispatch(p, s);
+    return ws_dispatch(p, s, launch);
 }
 
 }  // namespace zr

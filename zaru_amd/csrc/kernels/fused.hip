@@ -601,4 +601,10 @@ const char *launch_dwpw(const DwPwParams &p, hipStream_t s) {
     return launch_dwpw_mfma(p, s);
 }
 
+const char *launch_dwpw_group(const DwPwParams *p, int n, hipStream_t s) {
+    for (int i = 0; i < n; ++i)
+        if (valu_form(p[i])) return nullptr;
+    return launch_dwpw_mfma_group(p, n, s);
+}
+
 }  // namespace zr

@@ -14,21 +14,25 @@
 // Reference: the 1x1 Conv / Gemm nodes of the four ONNX graphs executed by ORT/tract at
 // crates/zaru/src/nn/mod.rs:483-533.
 #include "../runtime/zr_kernels.h"
+#include <algorithm>
 #include <cstdlib>
 #include "act.h"
 #include "epilogue.h"
+#include "group.h"
 
 namespace zr {
 
 constexpr int KC = 32;  // K rows per LDS stage
 
+// (the kernel bodies take their block coordinates as arguments: a grouped launch, group.h,
+// runs them for several parts of one grid)
 template <int MT, bool FULLPLANE>
-__global__ __launch_bounds__(256) void gemm_kernel(const GemmParams P) {
+__device__ __forceinline__ void gemm_body(const GemmParams &P, int bx, int by) {
     __shared__ float sW[KC][MT * 32];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int kh = lane >> 5, col = lane & 31;
-    const int m0 = blockIdx.y * (MT * 32);
-    const int j = (blockIdx.x * 4 + wave) * 32 + col;
+    const int m0 = by * (MT * 32);
+    const int j = (bx * 4 + wave) * 32 + col;
     const bool valid = j < P.ncols;
     const int jj = valid ? j : 0;
     const int n = jj / P.P, q = jj - n * P.P;
@@ -93,6 +97,17 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmParams P) {
     for (int t = 0; t < MT; ++t) epilogue_tile(P, acc[t], n, q, m0 + t * 32, kh);
 }
 
+template <int MT, bool FULLPLANE>
+__global__ __launch_bounds__(256) void gemm_kernel(const GemmParams P) {
+    gemm_body<MT, FULLPLANE>(P, blockIdx.x, blockIdx.y);
+}
+
+template <int MT, bool FULLPLANE>
+__global__ __launch_bounds__(256) void gemm_group_kernel(const LaunchGroup<GemmParams> G) {
+    const GroupSlot t = group_slot(G);
+    gemm_body<MT, FULLPLANE>(G.p[t.g], t.bx, t.by);
+}
+
 // Small-K form of gemm_kernel<1, false> (K <= NCH * 32, M <= 32: the FaceMesh tail's 128 -> 32
 // 1x1 convs over batch x 3x3 columns that the LDS-tiled form cannot take, ncols % 4 != 0).  Every
 // operand of the whole K extent is loaded up front in straight-line code (the weights straight
@@ -100,10 +115,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmParams P) {
 // per chunk (gemm_kernel stages each chunk through LDS behind two barriers).  The MFMA sequence
 // is gemm_kernel's, operand for operand, so the bits are too.
 template <int NCH>
-__global__ __launch_bounds__(256) void gemm_smallk_kernel(const GemmParams P) {
+__device__ __forceinline__ void gemm_smallk_body(const GemmParams &P, int bx) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int kh = lane >> 5, col = lane & 31;
-    const int j = (blockIdx.x * 4 + wave) * 32 + col;
+    const int j = (bx * 4 + wave) * 32 + col;
     const bool valid = j < P.ncols;
     const int jj = valid ? j : 0;
     const int n = jj / P.P, q = jj - n * P.P;
@@ -125,6 +140,17 @@ __global__ __launch_bounds__(256) void gemm_smallk_kernel(const GemmParams P) {
     epilogue_tile(P, acc, n, q, 0, kh);
 }
 
+template <int NCH>
+__global__ __launch_bounds__(256) void gemm_smallk_kernel(const GemmParams P) {
+    gemm_smallk_body<NCH>(P, blockIdx.x);
+}
+
+template <int NCH>
+__global__ __launch_bounds__(256) void gemm_smallk_group_kernel(const LaunchGroup<GemmParams> G) {
+    const GroupSlot t = group_slot(G);
+    gemm_smallk_body<NCH>(G.p[t.g], t.bx);
+}
+
 // ---------------------------------------------------------------- LDS-tiled variant
 // For the common case of a CNHW activation (X is then a plain row-major [K][ncols] matrix with
 // leading dimension x_sC) with ncols % 4 == 0: both operands are staged through LDS with
@@ -141,8 +167,7 @@ constexpr int TKC = 16;  // K rows per stage
 // (<1,1>: the skinny store-bound expand convs -- 4 waves per SIMD fit without spills and hide
 // more of the store latency than 3)
 template <int MT, int NT, bool RES>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MT * NT == 1 ? 4 : 1)))
-void gemm_tiled_kernel(const GemmParams P, int mblocks, int nct, int vec) {
+__device__ __forceinline__ void gemm_tiled_body(const GemmParams &P, int mblocks, int nct, int vec, int bx) {
     constexpr int BN = 4 * NT * 32, MR = MT * 32;
     constexpr int XV = TKC * BN / 4 / 256;  // float4 of X staged per thread per chunk
     constexpr int WV = (TKC * MR / 4 + 255) / 256;
@@ -151,10 +176,10 @@ void gemm_tiled_kernel(const GemmParams P, int mblocks, int nct, int vec) {
 
     int ct, mb;
     if (mblocks == 1) {
-        ct = blockIdx.x;
+        ct = bx;
         mb = 0;
     } else {
-        const int g = blockIdx.x / (8 * mblocks), r = blockIdx.x - g * 8 * mblocks;
+        const int g = bx / (8 * mblocks), r = bx - g * 8 * mblocks;
         mb = r >> 3;
         ct = g * 8 + (r & 7);
     }
@@ -267,6 +292,19 @@ void gemm_tiled_kernel(const GemmParams P, int mblocks, int nct, int vec) {
     }
 }
 
+template <int MT, int NT, bool RES>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MT * NT == 1 ? 4 : 1)))
+void gemm_tiled_kernel(const GemmParams P, int mblocks, int nct, int vec) {
+    gemm_tiled_body<MT, NT, RES>(P, mblocks, nct, vec, blockIdx.x);
+}
+
+template <int MT, int NT, bool RES>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MT * NT == 1 ? 4 : 1)))
+void gemm_tiled_group_kernel(const LaunchGroup<GemmParams> G) {
+    const GroupSlot t = group_slot(G);
+    gemm_tiled_body<MT, NT, RES>(G.p[t.g], G.a0[t.g], G.a1[t.g], G.a2[t.g], t.bx);
+}
+
 // ---------------------------------------------------------------- image-row variant
 // Full-plane convolutions on a 1-position output (the landmark heads: 3x3 conv over a 3x3
 // plane, M = 1404 / 1, K = Cin * 9) with the images as the GEMM's rows: C^T[n][m] =
@@ -281,12 +319,12 @@ void gemm_tiled_kernel(const GemmParams P, int mblocks, int nct, int vec) {
 // (vmcnt(0)) before each chunk's MFMAs, prefetched chunk included; straight-line code keeps the
 // next chunk's loads in flight.  Same k order, same bits.
 template <bool FULLPLANE, int NCH>
-__global__ __launch_bounds__(256) void gemm_rows_kernel(const GemmParams P, int mtiles) {
+__device__ __forceinline__ void gemm_rows_body(const GemmParams &P, int mtiles, int bx, int by) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int kh = lane >> 5, col = lane & 31;
-    const int mt = blockIdx.y * 4 + wave;
+    const int mt = by * 4 + wave;
     if (mt >= mtiles) return;  // no barriers in this kernel
-    const int m0 = mt * 32, n0 = blockIdx.x * 32;
+    const int m0 = mt * 32, n0 = bx * 32;
     const int nimg = P.ncols;  // P == 1: one column per image
     const int na = min(n0 + col, nimg - 1);
     const float *xa = P.x + (int64_t)na * P.x_sN;
@@ -355,51 +393,31 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(const GemmParams P, int 
     }
 }
 
-template <int MT, int NT>
-static const char *launch_tiled(const GemmParams &p, hipStream_t s) {
-    constexpr int BN = 4 * NT * 32;
-    const int nct = (p.ncols + BN - 1) / BN;
-    const int mblocks = (p.Mpad + MT * 32 - 1) / (MT * 32);
-    const int nblk = mblocks == 1 ? nct : ((nct + 7) / 8) * 8 * mblocks;
-    // 16-B output segments: whole 4-column groups inside one image, aligned rows
-    const int vec = form_on(FORM_VSTORE) && p.o_sP == 1 && p.P % 4 == 0 && p.o_sN % 4 == 0 &&
-                    p.o_sC % 4 == 0 && ((uintptr_t)p.out % 16) == 0;
-    // names as rocprofv3 prints the instance (bench.py joins the two by symbol)
-    static const char *names[2][2][5] = {
-        {{"", "gemm_tiled_kernel<1,1,false>", "gemm_tiled_kernel<2,1,false>", "gemm_tiled_kernel<3,1,false>", "gemm_tiled_kernel<4,1,false>"},
-         {"", "gemm_tiled_kernel<1,2,false>", "gemm_tiled_kernel<2,2,false>", "gemm_tiled_kernel<3,2,false>", "gemm_tiled_kernel<4,2,false>"}},
-        {{"", "gemm_tiled_kernel<1,1,true>", "gemm_tiled_kernel<2,1,true>", "gemm_tiled_kernel<3,1,true>", "gemm_tiled_kernel<4,1,true>"},
-         {"", "gemm_tiled_kernel<1,2,true>", "gemm_tiled_kernel<2,2,true>", "gemm_tiled_kernel<3,2,true>", "gemm_tiled_kernel<4,2,true>"}}};
-    if (p.res_mode == 0)
-        hipLaunchKernelGGL((gemm_tiled_kernel<MT, NT, false>), dim3(nblk), dim3(256), 0, s, p, mblocks, nct, vec);
-    else
-        hipLaunchKernelGGL((gemm_tiled_kernel<MT, NT, true>), dim3(nblk), dim3(256), 0, s, p, mblocks, nct, vec);
-    return names[p.res_mode != 0][NT - 1][MT];
+template <bool FULLPLANE, int NCH>
+__global__ __launch_bounds__(256) void gemm_rows_kernel(const GemmParams P, int mtiles) {
+    gemm_rows_body<FULLPLANE, NCH>(P, mtiles, blockIdx.x, blockIdx.y);
 }
 
-template <int NT>
-static const char *launch_tiled_nt(const GemmParams &p, int mt, hipStream_t s) {
-    switch (mt) {
-    case 4: return launch_tiled<4, NT>(p, s);
-    case 3: return launch_tiled<3, NT>(p, s);
-    case 2: return launch_tiled<2, NT>(p, s);
-    default: return launch_tiled<1, NT>(p, s);
-    }
+template <bool FULLPLANE, int NCH>
+__global__ __launch_bounds__(256) void gemm_rows_group_kernel(const LaunchGroup<GemmParams> G) {
+    const GroupSlot t = group_slot(G);
+    gemm_rows_body<FULLPLANE, NCH>(G.p[t.g], G.a0[t.g], t.bx, t.by);
 }
 
-template <int MT>
-static const char *launch_mt(const GemmParams &p, dim3 grid, hipStream_t s) {
-    static const char *names[2][5] = {
-        {"", "gemm_kernel<1,false>", "gemm_kernel<2,false>", "gemm_kernel<3,false>", "gemm_kernel<4,false>"},
-        {"", "gemm_kernel<1,true>", "gemm_kernel<2,true>", "gemm_kernel<3,true>", "gemm_kernel<4,true>"}};
-    if (p.KK > 1)
-        hipLaunchKernelGGL((gemm_kernel<MT, true>), grid, dim3(256), 0, s, p);
-    else
-        hipLaunchKernelGGL((gemm_kernel<MT, false>), grid, dim3(256), 0, s, p);
-    return names[p.KK > 1][MT];
-}
+// ---------------------------------------------------------------- launch choice
+// The form, template variant, grid and scalar arguments launch_gemm picks for a GEMM; grouped
+// launches use it to check that sibling steps would run the same kernel instance.
+enum GemmForm { GF_GENERIC, GF_TILED, GF_ROWS, GF_SMALLK };
+struct GemmChoice {
+    GemmForm form;
+    int v0 = 0, v1 = 0, v2 = 0;  // generic: MT, FULLPLANE; tiled: MT, NT, RES; rows: NCH; smallk: NCH
+    int gx = 1, gy = 1;
+    int a0 = 0, a1 = 0, a2 = 0;  // tiled: mblocks, nct, vec; rows: mtiles
+    bool same_instance(const GemmChoice &o) const { return form == o.form && v0 == o.v0 && v1 == o.v1 && v2 == o.v2; }
+};
 
-const char *launch_gemm(const GemmParams &p, hipStream_t s) {
+static GemmChoice choose_gemm(const GemmParams &p) {
+    GemmChoice c{};
     const int mtiles = p.Mpad / 32;
     // LDS-tiled path: X must be a row-major [K][ncols] matrix with 16-B aligned rows
     const bool rowmajor = p.KK == 1 && p.x_sN == p.P && (p.x_sC % 4) == 0 && (p.ncols % 4) == 0 &&
@@ -413,37 +431,150 @@ const char *launch_gemm(const GemmParams &p, hipStream_t s) {
         const int bn = 4 * nt * 32;
         // keep >= ~2 workgroups per CU: trade M-tile reuse for parallelism on small problems
         while (mt > 1 && (int64_t)((p.ncols + bn - 1) / bn) * ((mtiles + mt - 1) / mt) < 512) --mt;
-        return nt == 2 ? launch_tiled_nt<2>(p, mt, s) : launch_tiled_nt<1>(p, mt, s);
+        mt = std::max(mt, 1);
+        const int nct = (p.ncols + bn - 1) / bn;
+        const int mblocks = (p.Mpad + mt * 32 - 1) / (mt * 32);
+        // 16-B output segments: whole 4-column groups inside one image, aligned rows
+        const int vec = form_on(FORM_VSTORE) && p.o_sP == 1 && p.P % 4 == 0 && p.o_sN % 4 == 0 &&
+                        p.o_sC % 4 == 0 && ((uintptr_t)p.out % 16) == 0;
+        c.form = GF_TILED;
+        c.v0 = mt, c.v1 = nt, c.v2 = p.res_mode != 0;
+        c.gx = mblocks == 1 ? nct : ((nct + 7) / 8) * 8 * mblocks;
+        c.a0 = mblocks, c.a1 = nct, c.a2 = vec;
+        return c;
     }
     if (p.P == 1 && p.res_mode == 0 && p.KK > 1 && form_on(FORM_ROWS)) {  // a head over whole planes (KK >= 2)
-        dim3 grid((p.ncols + 31) / 32, (mtiles + 3) / 4);
-        if ((p.Kpad + KC - 1) / KC == 9) {
-            hipLaunchKernelGGL((gemm_rows_kernel<true, 9>), grid, dim3(256), 0, s, p, mtiles);
-            return "gemm_rows_kernel<true, 9>";
-        }
-        hipLaunchKernelGGL((gemm_rows_kernel<true, 0>), grid, dim3(256), 0, s, p, mtiles);
-        return "gemm_rows_kernel<true, 0>";
+        c.form = GF_ROWS;
+        c.v0 = (p.Kpad + KC - 1) / KC == 9 ? 9 : 0;
+        c.gx = (p.ncols + 31) / 32, c.gy = (mtiles + 3) / 4;
+        c.a0 = mtiles;
+        return c;
     }
     const int bx = (p.ncols + 127) / 128;
     const int nch = (p.Kpad + KC - 1) / KC;
     if (p.KK == 1 && mtiles == 1 && nch <= 4 && form_on(FORM_ROWS)) {
-        switch (nch) {
-        case 1: hipLaunchKernelGGL((gemm_smallk_kernel<1>), dim3(bx), dim3(256), 0, s, p); return "gemm_smallk_kernel<1>";
-        case 2: hipLaunchKernelGGL((gemm_smallk_kernel<2>), dim3(bx), dim3(256), 0, s, p); return "gemm_smallk_kernel<2>";
-        case 3: hipLaunchKernelGGL((gemm_smallk_kernel<3>), dim3(bx), dim3(256), 0, s, p); return "gemm_smallk_kernel<3>";
-        default: hipLaunchKernelGGL((gemm_smallk_kernel<4>), dim3(bx), dim3(256), 0, s, p); return "gemm_smallk_kernel<4>";
-        }
+        c.form = GF_SMALLK;
+        c.v0 = std::max(nch, 1);
+        c.gx = bx;
+        return c;
     }
     // Largest M tile (operand reuse) that still leaves >= 2 workgroups per CU of parallelism.
     int mt = 4;
     while (mt > 1 && (int64_t)bx * ((mtiles + mt - 1) / mt) < 512) --mt;
     if (mt > mtiles) mt = mtiles;
-    dim3 grid(bx, (mtiles + mt - 1) / mt);
-    switch (mt) {
-    case 4: return launch_mt<4>(p, grid, s);
-    case 3: return launch_mt<3>(p, grid, s);
-    case 2: return launch_mt<2>(p, grid, s);
-    default: return launch_mt<1>(p, grid, s);
+    mt = std::max(mt, 1);
+    c.form = GF_GENERIC;
+    c.v0 = mt, c.v1 = p.KK > 1;
+    c.gx = bx, c.gy = (mtiles + mt - 1) / mt;
+    return c;
+}
+
+// names as rocprofv3 prints the instance (bench.py joins the two by symbol)
+template <int MT, int NT, bool RES>
+static const char *launch_tiled(const GemmParams &p, const GemmChoice &c, hipStream_t s) {
+    hipLaunchKernelGGL((gemm_tiled_kernel<MT, NT, RES>), dim3(c.gx), dim3(256), 0, s, p, c.a0, c.a1, c.a2);
+    return kernel_name("gemm_tiled_kernel<%d,%d,%s>", MT, NT, RES ? "true" : "false");
+}
+
+template <int NT, bool RES>
+static const char *launch_tiled_mt(const GemmParams &p, const GemmChoice &c, hipStream_t s) {
+    switch (c.v0) {
+    case 4: return launch_tiled<4, NT, RES>(p, c, s);
+    case 3: return launch_tiled<3, NT, RES>(p, c, s);
+    case 2: return launch_tiled<2, NT, RES>(p, c, s);
+    default: return launch_tiled<1, NT, RES>(p, c, s);
+    }
+}
+
+template <int MT>
+static const char *launch_mt(const GemmParams &p, const GemmChoice &c, hipStream_t s) {
+    const dim3 grid(c.gx, c.gy);
+    if (c.v1) hipLaunchKernelGGL((gemm_kernel<MT, true>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((gemm_kernel<MT, false>), grid, dim3(256), 0, s, p);
+    return kernel_name("gemm_kernel<%d,%s>", MT, c.v1 ? "true" : "false");
+}
+
+const char *launch_gemm(const GemmParams &p, hipStream_t s) {
+    const GemmChoice c = choose_gemm(p);
+    switch (c.form) {
+    case GF_TILED:
+        if (c.v1 == 2) return c.v2 ? launch_tiled_mt<2, true>(p, c, s) : launch_tiled_mt<2, false>(p, c, s);
+        return c.v2 ? launch_tiled_mt<1, true>(p, c, s) : launch_tiled_mt<1, false>(p, c, s);
+    case GF_ROWS:
+        if (c.v0 == 9) {
+            hipLaunchKernelGGL((gemm_rows_kernel<true, 9>), dim3(c.gx, c.gy), dim3(256), 0, s, p, c.a0);
+            return "gemm_rows_kernel<true, 9>";
+        }
+        hipLaunchKernelGGL((gemm_rows_kernel<true, 0>), dim3(c.gx, c.gy), dim3(256), 0, s, p, c.a0);
+        return "gemm_rows_kernel<true, 0>";
+    case GF_SMALLK:
+        switch (c.v0) {
+        case 1: hipLaunchKernelGGL((gemm_smallk_kernel<1>), dim3(c.gx), dim3(256), 0, s, p); return "gemm_smallk_kernel<1>";
+        case 2: hipLaunchKernelGGL((gemm_smallk_kernel<2>), dim3(c.gx), dim3(256), 0, s, p); return "gemm_smallk_kernel<2>";
+        case 3: hipLaunchKernelGGL((gemm_smallk_kernel<3>), dim3(c.gx), dim3(256), 0, s, p); return "gemm_smallk_kernel<3>";
+        default: hipLaunchKernelGGL((gemm_smallk_kernel<4>), dim3(c.gx), dim3(256), 0, s, p); return "gemm_smallk_kernel<4>";
+        }
+    default:
+        switch (c.v0) {
+        case 4: return launch_mt<4>(p, c, s);
+        case 3: return launch_mt<3>(p, c, s);
+        case 2: return launch_mt<2>(p, c, s);
+        default: return launch_mt<1>(p, c, s);
+        }
+    }
+}
+
+// Sibling GEMMs in one launch when every part would run the same kernel instance and that
+// instance has a grouped form (the ones the plans' sibling steps use: the hand heads' generic /
+// tiled 1-tile GEMMs, the FaceMesh heads' row form and small-K 1x1s); nullptr otherwise.
+const char *launch_gemm_group(const GemmParams *p, int n, hipStream_t s) {
+    if (n < 2 || n > ZR_GROUP_MAX) return nullptr;
+    GemmChoice c[ZR_GROUP_MAX];
+    for (int i = 0; i < n; ++i) {
+        c[i] = choose_gemm(p[i]);
+        if (!c[i].same_instance(c[0])) return nullptr;
+    }
+    const GemmChoice &c0 = c[0];
+    const bool ok = (c0.form == GF_GENERIC && c0.v0 == 1) || (c0.form == GF_TILED && c0.v0 == 1 && c0.v1 == 1 && !c0.v2) ||
+                    c0.form == GF_ROWS || c0.form == GF_SMALLK;
+    if (!ok) return nullptr;
+    LaunchGroup<GemmParams> G{};
+    G.n = n;
+    int total = 0;
+    for (int i = 0; i < n; ++i) {
+        G.p[i] = p[i];
+        G.a0[i] = c[i].a0, G.a1[i] = c[i].a1, G.a2[i] = c[i].a2;
+        G.gx[i] = c[i].gx;
+        G.start[i] = total;
+        total += c[i].gx * c[i].gy;
+    }
+    for (int i = n; i <= ZR_GROUP_MAX; ++i) G.start[i] = total;
+    const dim3 grid(total), block(256);
+    switch (c0.form) {
+    case GF_TILED:
+        hipLaunchKernelGGL((gemm_tiled_group_kernel<1, 1, false>), grid, block, 0, s, G);
+        return "gemm_tiled_group_kernel<1,1,false>";
+    case GF_ROWS:
+        if (c0.v0 == 9) {
+            hipLaunchKernelGGL((gemm_rows_group_kernel<true, 9>), grid, block, 0, s, G);
+            return "gemm_rows_group_kernel<true, 9>";
+        }
+        hipLaunchKernelGGL((gemm_rows_group_kernel<true, 0>), grid, block, 0, s, G);
+        return "gemm_rows_group_kernel<true, 0>";
+    case GF_SMALLK:
+        switch (c0.v0) {
+        case 1: hipLaunchKernelGGL((gemm_smallk_group_kernel<1>), grid, block, 0, s, G); return "gemm_smallk_group_kernel<1>";
+        case 2: hipLaunchKernelGGL((gemm_smallk_group_kernel<2>), grid, block, 0, s, G); return "gemm_smallk_group_kernel<2>";
+        case 3: hipLaunchKernelGGL((gemm_smallk_group_kernel<3>), grid, block, 0, s, G); return "gemm_smallk_group_kernel<3>";
+        default: hipLaunchKernelGGL((gemm_smallk_group_kernel<4>), grid, block, 0, s, G); return "gemm_smallk_group_kernel<4>";
+        }
+    default:
+        if (c0.v1) {
+            hipLaunchKernelGGL((gemm_group_kernel<1, true>), grid, block, 0, s, G);
+            return "gemm_group_kernel<1,true>";
+        }
+        hipLaunchKernelGGL((gemm_group_kernel<1, false>), grid, block, 0, s, G);
+        return "gemm_group_kernel<1,false>";
     }
 }
 

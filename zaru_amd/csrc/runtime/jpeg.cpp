@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -272,6 +273,9 @@ struct zr_jpeg_decoder {
     // bytes staged in pinned memory and copied once per frame
     uint8_t *h_stage = nullptr, *d_stage = nullptr;
     size_t stage_cap = 0;
+    // self-synchronising device decoding (streams without restart intervals): per-segment states
+    uint8_t *d_sync = nullptr;
+    size_t sync_cap = 0;
     int *d_err = nullptr;         // [4096] per frame of the last call: set by jpeg_huff_kernel on a corrupt interval
     size_t n_last = 0;            // frames of the last call
     uint64_t n_gpu = 0, n_host = 0;
@@ -426,6 +430,14 @@ bool unstuff_intervals(const uint8_t *d, size_t n, size_t begin, int n_iv, uint8
     return (int)off.size() == n_iv + 1;
 }
 
+bool sync_entropy_enabled() {  // ZARU_JPEG_SYNC=0: streams without DRI decode on the host (A/B)
+    static const bool on = [] {
+        const char *e = std::getenv("ZARU_JPEG_SYNC");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 bool gpu_entropy_enabled() {  // ZARU_JPEG_HOST_ENTROPY=1 keeps every decode on the host (A/B)
     static const bool on = [] {
         const char *e = std::getenv("ZARU_JPEG_HOST_ENTROPY");
@@ -479,6 +491,7 @@ void zr_jpeg_decoder_destroy(zr_jpeg_decoder *d) {
     (void)hipFree(d->d_planes);
     (void)hipHostFree(d->h_stage);
     (void)hipFree(d->d_stage);
+    (void)hipFree(d->d_sync);
     (void)hipFree(d->d_err);
     delete d;
 }
@@ -615,16 +628,50 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
             ob[f] = ((size_t)(n_iv[f] + 1) * 4 + 15) / 16 * 16;
             groups += (size_t)(n_iv[f] + 63) / 64;
         }
+        // streams without restart intervals: self-synchronising decoding (jpeg_sync.hip), its
+        // staged scan padded to whole 64-segment workgroup ranges + the overrun margin
+        std::vector<char> sync(n, 0);
+        std::vector<size_t> sofs(n, 0), spad(n, 0);
+        size_t nsync = 0, sgroups = 0;
+        for (size_t f = 0; f < n; f++) {
+            if (!gpu_entropy_enabled() || !sync_entropy_enabled() || hd[f].restart != 0) continue;
+            const size_t bound = lens[f] - hd[f].scan_begin;
+            const size_t nseg = (bound * 8 + zr::JS_SEG - 1) / zr::JS_SEG;
+            if (nseg == 0 || bound * 8 >= ((size_t)1 << 30)) continue;
+            // scans of > JS_MAX_BITS_PER_BLOCK bits per block on average (near-lossless noise) fall
+            // into step too slowly for the sync passes (measured: q100 noise, ~700 bits per block,
+            // still had chains after 32 passes): the host decodes them
+            int bpm_f = 0;
+            for (int c = 0; c < hd[f].ncomp; c++) bpm_f += hd[f].comp[c].h * hd[f].comp[c].v;
+            if ((int64_t)bound * 8 > (int64_t)zr::JS_MAX_BITS_PER_BLOCK * nmcu[f] * bpm_f) continue;
+            sync[f] = 1;
+            nsync++;
+            sgroups += (nseg + zr::JS_LANES - 1) / zr::JS_LANES;
+            spad[f] = (nseg + zr::JS_LANES - 1) / zr::JS_LANES * zr::JS_LANES * (zr::JS_SEG / 8) + zr::JS_MARGIN +
+                      zr::JS_WARM_MAX / 8 + 16;  // (the first workgroup stages its warm-up's worth past the rest)
+        }
         const size_t fb = (n * sizeof(zr::JpegHuffFrame) + 15) / 16 * 16, wb = (groups * 8 + 15) / 16 * 16;
-        stage = fb + wb;
+        const size_t sfb = (nsync * sizeof(zr::JpegSyncFrame) + 15) / 16 * 16, swb = (sgroups * 8 + 15) / 16 * 16;
+        stage = fb + wb + sfb + swb;
         for (size_t f = 0; f < n; f++)
             if (n_iv[f]) {
                 fofs[f] = stage;
                 stage += tb + ob[f] + ((lens[f] - hd[f].scan_begin) + 48 + 15) / 16 * 16;
+            } else if (sync[f]) {
+                sofs[f] = stage;
+                stage += tb + spad[f];
             }
         // growing frees device buffers: the previous decode's kernels must be done with them
+        // per-segment device states of the sync frames (ck, exits x2, start, base, pred) + err_block
+        size_t sync_bytes = 0;
+        for (size_t f = 0; f < n; f++)
+            if (sync[f]) {
+                const size_t nseg = (spad[f] - zr::JS_MARGIN - zr::JS_WARM_MAX / 8 - 16) / (zr::JS_SEG / 8);
+                sync_bytes += nseg * (zr::JS_CK * sizeof(zr::JpegSyncState) + sizeof(zr::JpegSyncState) + 8 + 4 + 12) + 16;
+            }
+        if (sync_bytes) sync_bytes += 256;  // the per-pass change counters
         const bool grow = (size_t)blocks > dec->coef_cap || (size_t)pbytes > dec->planes_cap ||
-                          (groups && stage > dec->stage_cap);
+                          ((groups || nsync) && stage > dec->stage_cap) || sync_bytes > dec->sync_cap;
         if (grow && hipEventSynchronize(dec->done) != hipSuccess) return err(ZR_ERR_DEVICE, "event sync failed");
         if ((size_t)blocks > dec->coef_cap) {
             (void)hipHostFree(dec->h_coef);
@@ -646,7 +693,15 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
             if (hipMalloc((void **)&dec->d_planes, cap) != hipSuccess) return err(ZR_ERR_DEVICE, "jpeg: out of memory");
             dec->planes_cap = cap;
         }
-        if (groups && stage > dec->stage_cap) {
+        if (sync_bytes > dec->sync_cap) {
+            (void)hipFree(dec->d_sync);
+            dec->d_sync = nullptr;
+            dec->sync_cap = 0;
+            const size_t cap = sync_bytes + sync_bytes / 4;
+            if (hipMalloc((void **)&dec->d_sync, cap) != hipSuccess) return err(ZR_ERR_DEVICE, "jpeg: out of memory");
+            dec->sync_cap = cap;
+        }
+        if ((groups || nsync) && stage > dec->stage_cap) {
             (void)hipHostFree(dec->h_stage);
             (void)hipFree(dec->d_stage);
             dec->h_stage = nullptr;
@@ -664,7 +719,7 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
         int lds = 0;
         auto *fr = reinterpret_cast<zr::JpegHuffFrame *>(dec->h_stage);
         auto *wg = reinterpret_cast<int32_t *>(dec->h_stage + fb);
-        size_t n_wg = 0, used = fb + wb;
+        size_t n_wg = 0, used = fb + wb + sfb + swb;
         for (size_t f = 0; f < n; f++) {
             if (!n_iv[f]) continue;
             uint8_t *const base = dec->h_stage + fofs[f];
@@ -715,11 +770,88 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
                 wg[2 * n_wg + 1] = g0;
                 n_wg++;
             }
-            used = fofs[f] + tb + ob[f] + (db + 48 + 15) / 16 * 16;
+            used = std::max(used, fofs[f] + tb + ob[f] + (db + 48 + 15) / 16 * 16);
+        }
+        // the sync frames: unstuffed scans, tables, per-segment state arrays, workgroup list
+        auto *sfr = reinterpret_cast<zr::JpegSyncFrame *>(dec->h_stage + fb + wb);
+        auto *swg = reinterpret_cast<int32_t *>(dec->h_stage + fb + wb + sfb);
+        size_t ns = 0, n_swg = 0, sy = 256;  // [0, 256): the change counters
+        int sync_lds = 0;
+        for (size_t f = 0; f < n; f++) {
+            if (!sync[f]) continue;
+            uint8_t *const base = dec->h_stage + sofs[f];
+            std::vector<int32_t> one;
+            if (!unstuff_intervals(jpegs[f], lens[f], hd[f].scan_begin, 1, base + tb, one)) {
+                sync[f] = 0;  // markers inside the scan: the host decoder reports what they are
+                continue;
+            }
+            const size_t nbytes = (size_t)one.back();
+            const int nseg = std::max(1, (int)((nbytes * 8 + zr::JS_SEG - 1) / zr::JS_SEG));
+            std::memset(base + tb + nbytes, 0, spad[f] - nbytes);
+            auto *tabs = reinterpret_cast<zr::JpegHuffTable *>(base);
+            for (int t = 0; t < 4; t++) {
+                dev_table(hd[f].dc[t], tabs[t]);
+                dev_table(hd[f].ac[t], tabs[4 + t]);
+            }
+            uint8_t *const dbase = dec->d_stage + sofs[f];
+            zr::JpegSyncFrame &F = sfr[ns];
+            F = zr::JpegSyncFrame{};
+            F.tables = reinterpret_cast<const zr::JpegHuffTable *>(dbase);
+            F.data = dbase + tb;
+            F.nbytes = (int)nbytes;
+            F.nbits = (int)nbytes * 8;
+            F.nseg = nseg;
+            F.mcux = mcux[f];
+            F.ncomp = hd[f].ncomp;
+            int u = 0;
+            for (int c = 0; c < hd[f].ncomp; c++) {
+                F.ch[c] = hd[f].comp[c].h;
+                F.cv[c] = hd[f].comp[c].v;
+                F.td[c] = hd[f].comp[c].td;
+                F.ta[c] = hd[f].comp[c].ta;
+                F.coef_off[c] = P[f].coef_off[c];
+                F.bw[c] = P[f].bw[c];
+                for (int v = 0; v < F.cv[c]; v++)
+                    for (int h = 0; h < F.ch[c]; h++) {
+                        F.ucomp[u] = c;
+                        F.uby[u] = v;
+                        F.ubx[u] = h;
+                        u++;
+                    }
+            }
+            F.bpm = u;
+            F.nblocks = nmcu[f] * u;
+            // warm-up: ~12 average blocks (high-rate scans fall into step over more bits)
+            const int64_t bpb = (int64_t)F.nbits / std::max(1, F.nblocks);
+            F.warm = (int)std::min<int64_t>(zr::JS_WARM_MAX, std::max<int64_t>(zr::JS_WARM_MIN, (12 * bpb + 127) / 128 * 128));
+            sync_lds = std::max(sync_lds, F.warm / 8 + zr::JS_LANES * (zr::JS_SEG / 8) + zr::JS_MARGIN);
+            F.coef = dec->d_coef + cofs[f] * 64;
+            F.frame = (int)f;
+            uint8_t *sp = dec->d_sync + sy;
+            F.ck = reinterpret_cast<zr::JpegSyncState *>(sp);
+            sp += (size_t)nseg * zr::JS_CK * sizeof(zr::JpegSyncState);
+            F.x = reinterpret_cast<zr::JpegSyncState *>(sp);
+            sp += (size_t)nseg * sizeof(zr::JpegSyncState);
+            F.start = reinterpret_cast<int2 *>(sp);
+            sp += (size_t)nseg * 8;
+            F.base = reinterpret_cast<int32_t *>(sp);
+            sp += (size_t)nseg * 4;
+            F.pred = reinterpret_cast<int32_t *>(sp);
+            sp += (size_t)nseg * 12;
+            F.err_block = reinterpret_cast<int32_t *>(sp);
+            sp += 16;
+            sy = (size_t)(sp - dec->d_sync);
+            for (int g0 = 0; g0 < nseg; g0 += zr::JS_LANES) {
+                swg[2 * n_swg] = (int32_t)ns;
+                swg[2 * n_swg + 1] = g0;
+                n_swg++;
+            }
+            used = std::max(used, sofs[f] + tb + spad[f]);
+            ns++;
         }
         // host entropy decoding for the rest, into their slots of the pinned coefficient staging
         for (size_t f = 0; f < n; f++)
-            if (!n_iv[f]) {
+            if (!n_iv[f] && !sync[f]) {
                 try {
                     entropy_decode(hd[f], P[f], jpegs[f], lens[f], dec->h_coef + cofs[f] * 64);
                 } catch (const JpegError &e) {
@@ -731,10 +863,10 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
         hipStream_t st = (hipStream_t)hip_stream;
         if (hipStreamWaitEvent(st, dec->done, 0) != hipSuccess) return err(ZR_ERR_DEVICE, "jpeg: stream wait failed");
         for (size_t f = 0; f < n; f++)
-            if (!n_iv[f] && hipMemcpyAsync(dec->d_coef + cofs[f] * 64, dec->h_coef + cofs[f] * 64,
+            if (!n_iv[f] && !sync[f] && hipMemcpyAsync(dec->d_coef + cofs[f] * 64, dec->h_coef + cofs[f] * 64,
                                            (size_t)P[f].total_blocks * 128, hipMemcpyHostToDevice, st) != hipSuccess)
                 return err(ZR_ERR_DEVICE, "jpeg: coefficient upload failed");
-        if (n_wg && hipMemcpyAsync(dec->d_stage, dec->h_stage, used, hipMemcpyHostToDevice, st) != hipSuccess)
+        if ((n_wg || ns) && hipMemcpyAsync(dec->d_stage, dec->h_stage, used, hipMemcpyHostToDevice, st) != hipSuccess)
             return err(ZR_ERR_DEVICE, "jpeg: scan upload failed");
         if (hipEventRecord(dec->staged, st) != hipSuccess) return err(ZR_ERR_DEVICE, "jpeg: event record failed");
         // this call's per-frame error flags (the device decode reports corruption asynchronously)
@@ -750,13 +882,50 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
             hp.lds_bytes = lds;
             zr::launch_jpeg_huff(hp, st);
         }
+        if (ns) {
+            zr::JpegSyncParams sp{};
+            sp.frames = reinterpret_cast<const zr::JpegSyncFrame *>(dec->d_stage + fb + wb);
+            sp.wg = reinterpret_cast<const int32_t *>(dec->d_stage + fb + wb + sfb);
+            sp.n_wg = (int)n_swg;
+            sp.nframes = (int)ns;
+            sp.error = dec->d_err;
+            sp.lds_bytes = sync_lds;
+            sp.changed = reinterpret_cast<int *>(dec->d_sync);
+            static_assert((zr::JS_PASSES + 1) * sizeof(int) <= 256, "change counters");
+            if (hipMemsetAsync(dec->d_sync, 0, 256, st) != hipSuccess) return err(ZR_ERR_DEVICE, "jpeg: counter reset failed");
+            for (int pass = 0; pass <= zr::JS_PASSES; pass++) zr::launch_jpeg_sync_scan(sp, pass, st);
+            zr::launch_jpeg_sync_finish(sp, st);
+            if (const char *dump = std::getenv("ZARU_JPEG_SYNC_DUMP")) {  // diagnostics: the first sync frame's states
+                const zr::JpegSyncFrame &F0 = sfr[0];
+                std::vector<int> cnt(64);
+                std::vector<zr::JpegSyncState> xs(F0.nseg);
+                std::vector<int2> starts(F0.nseg);
+                std::vector<int32_t> bases(F0.nseg);
+                int eb = 0;
+                (void)hipStreamSynchronize(st);
+                (void)hipMemcpy(cnt.data(), dec->d_sync, 256, hipMemcpyDeviceToHost);
+                (void)hipMemcpy(xs.data(), F0.x, xs.size() * sizeof(zr::JpegSyncState), hipMemcpyDeviceToHost);
+                (void)hipMemcpy(starts.data(), F0.start, starts.size() * 8, hipMemcpyDeviceToHost);
+                (void)hipMemcpy(bases.data(), F0.base, bases.size() * 4, hipMemcpyDeviceToHost);
+                (void)hipMemcpy(&eb, F0.err_block, 4, hipMemcpyDeviceToHost);
+                if (FILE *fp = std::fopen(dump, "w")) {
+                    std::fprintf(fp, "nseg %d nblocks %d warm %d err_block %d\nchanged", F0.nseg, F0.nblocks, F0.warm, eb);
+                    for (int i = 0; i <= zr::JS_PASSES; i++) std::fprintf(fp, " %d", cnt[i]);
+                    std::fprintf(fp, "\n");
+                    for (int i = 0; i < F0.nseg; i++)
+                        std::fprintf(fp, "%d start %d %d exit %d %d nblk %d err %d base %d\n", i, starts[i].x, starts[i].y,
+                                     xs[i].pos, xs[i].u, xs[i].nblk, xs[i].err, bases[i]);
+                    std::fclose(fp);
+                }
+            }
+        }
         for (size_t f = 0; f < n; f++) {
             P[f].coef = dec->d_coef + cofs[f] * 64;
             P[f].planes = dec->d_planes;
             P[f].out = d_rgba[f];
             P[f].out_stride = (int64_t)row_strides[f];
             zr::launch_jpeg(P[f], st);
-            if (n_iv[f])
+            if (n_iv[f] || sync[f])
                 dec->n_gpu++;
             else
                 dec->n_host++;

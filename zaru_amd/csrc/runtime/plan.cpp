@@ -82,6 +82,8 @@ class Compiler {
     }
     bool act_from_node(const OnnxNode &nd, int C, int Cpad, ActDesc &a);
     void finalize_outputs();
+    void fuse_dw_gap();
+    void group_siblings();
     void allocate();
 };
 
@@ -850,16 +852,130 @@ bool Compiler::lower() {
     return true;
 }
 
+// Launch grouping: sibling steps that do not depend on each other and would run the same kernel
+// instance (the FaceMesh flag and mesh branches after the 6^2 trunk, the four hand-landmark
+// heads over the pooled features) are scheduled next to each other and launched as one grid
+// (kernels/group.h).  A list schedule in plan order: a step with no ready partner but one later
+// in the plan waits while ready steps without any prospective partner run first, so the two
+// FaceMesh branches line up layer by layer.  Runs before allocate(), which gives the members of
+// a group one shared time step (they run concurrently).
+static bool groupable(const Step &a, const Step &b) {
+    if (a.kind != b.kind || a.in.kind == 1 || b.in.kind == 1) return false;
+    if (a.kind == S_DWPW)
+        return a.kh == b.kh && a.stride == b.stride && a.pad_t == b.pad_t && a.pad_l == b.pad_l &&
+               a.in.H == b.in.H && a.in.W == b.in.W && a.out.H == b.out.H && a.out.W == b.out.W &&
+               a.K == b.K && a.Mpad == b.Mpad;
+    if (a.kind == S_GEMM)
+        return a.KK == b.KK && a.K == b.K && a.kh == b.kh && a.kw == b.kw && a.stride == b.stride &&
+               a.in.C == b.in.C && a.in.H == b.in.H && a.in.W == b.in.W && a.out.H == b.out.H &&
+               a.out.W == b.out.W;  // (M may differ: the launch checks the parts' kernel instance)
+    return false;
+}
+
+// A global average pool over a depthwise conv's output, which nothing else reads, folds into
+// the depthwise launch (dwgap_kernel): the hand landmark network's 672 x 7^2 tail.
+void Compiler::fuse_dw_gap() {
+    for (size_t gi = 0; gi < P.steps.size(); ++gi) {
+        Step &g = P.steps[gi];
+        if (g.kind != S_GAP || g.in.kind != 0 || g.in.c_off != 0) continue;
+        int prod = -1, readers = 0;
+        for (size_t i = 0; i < P.steps.size(); ++i) {
+            const Step &s = P.steps[i];
+            if (s.out.kind == 0 && s.out.id == g.in.id) prod = prod < 0 ? (int)i : -2;
+            for (const TRef *r : {&s.in, &s.in2})
+                if (r->kind == 0 && r->id == g.in.id) ++readers;
+        }
+        if (prod < 0 || readers != 1) continue;
+        Step &d = P.steps[prod];
+        if (d.kind != S_DW || (d.kh != 3 && d.kh != 5) || d.kh != d.kw || (int64_t)d.in.H * d.in.W > 512) continue;
+        d.kind = S_DWGAP;
+        d.dw_oh = d.out.H;
+        d.dw_ow = d.out.W;
+        d.name += "+" + g.name;
+        d.out = g.out;
+        d.bytes = 4.0 * ((double)d.in.C * d.in.H * d.in.W + d.in.C);
+        P.steps.erase(P.steps.begin() + gi);
+        --gi;
+    }
+}
+
+void Compiler::group_siblings() {
+    const int n = (int)P.steps.size();
+    if (n < 2) return;
+    auto touches = [](const TRef &r, const TRef &w) {  // same storage (internal) or same graph output
+        return r.kind == w.kind && r.kind != 1 && r.id >= 0 && r.id == w.id;
+    };
+    // dep[j][i]: j must run after i (reads what i writes, writes what i reads or writes)
+    std::vector<std::vector<char>> dep(n, std::vector<char>(n, 0));
+    for (int j = 0; j < n; ++j)
+        for (int i = 0; i < j; ++i) {
+            const Step &a = P.steps[i], &b = P.steps[j];
+            bool d = touches(b.in, a.out) || touches(b.out, a.out) || touches(b.out, a.in);
+            if (b.res_mode || b.kind == S_ELT) d = d || touches(b.in2, a.out);
+            if (a.res_mode || a.kind == S_ELT) d = d || touches(b.out, a.in2);
+            dep[j][i] = d;
+        }
+    // transitive closure: related[i][j] = one of them (transitively) depends on the other
+    std::vector<std::vector<char>> anc = dep;
+    for (int j = 0; j < n; ++j)
+        for (int i = 0; i < j; ++i)
+            if (anc[j][i])
+                for (int k = 0; k < i; ++k) anc[j][k] |= anc[i][k];
+    auto related = [&](int a, int b) { return a < b ? anc[b][a] : anc[a][b]; };
+    std::vector<char> done(n, 0);
+    auto ready = [&](int j) {
+        if (done[j]) return false;
+        for (int i = 0; i < j; ++i)
+            if (dep[j][i] && !done[i]) return false;
+        return true;
+    };
+    auto future_partner = [&](int s) {
+        for (int t = 0; t < n; ++t)
+            if (t != s && !done[t] && !ready(t) && !related(s, t) && groupable(P.steps[s], P.steps[t])) return true;
+        return false;
+    };
+    std::vector<Step> out;
+    out.reserve(n);
+    for (int left = n; left > 0;) {
+        std::vector<int> rd;
+        for (int j = 0; j < n; ++j)
+            if (ready(j)) rd.push_back(j);
+        auto partners_of = [&](int s) {
+            std::vector<int> g{s};
+            for (int t : rd)
+                if (t != s && (int)g.size() < ZR_GROUP_MAX && groupable(P.steps[s], P.steps[t])) g.push_back(t);
+            return g;
+        };
+        std::vector<int> g = partners_of(rd[0]);
+        if (g.size() == 1 && future_partner(rd[0]))
+            for (int r : rd)
+                if (r != rd[0] && !future_partner(r)) {
+                    g = partners_of(r);
+                    break;
+                }
+        for (size_t k = 0; k < g.size(); ++k) {
+            Step st = P.steps[g[k]];
+            st.group = k == 0 ? (int)g.size() : 0;
+            out.push_back(std::move(st));
+            done[g[k]] = 1;
+        }
+        left -= (int)g.size();
+    }
+    P.steps = std::move(out);
+}
+
 void Compiler::allocate() {
-    // liveness over step indices
+    // liveness over launch times (the members of a launch group share one)
     const size_t ns = P.storage_size.size();
     std::vector<int> first(ns, 1 << 30), last(ns, -1);
+    int time = -1;
     for (size_t i = 0; i < P.steps.size(); i++) {
         const Step &s = P.steps[i];
+        if (s.group != 0) ++time;
         for (const TRef *r : {&s.in, &s.in2, &s.out})
             if (r->kind == 0 && r->id >= 0) {
-                first[r->id] = std::min(first[r->id], (int)i);
-                last[r->id] = std::max(last[r->id], (int)i);
+                first[r->id] = std::min(first[r->id], time);
+                last[r->id] = std::max(last[r->id], time);
             }
     }
     std::vector<int> order(ns);
@@ -954,6 +1070,8 @@ bool Compiler::run(const std::vector<uint32_t> &sel) {
                 reader = (int)i;
             }
     P.input_fusable = readers == 1 && P.steps[reader].kind == S_DIRECT && P.steps[reader].stem;
+    if (form_on(FORM_DWGAP)) fuse_dw_gap();
+    if (form_on(FORM_GROUPS)) group_siblings();
     allocate();
     return true;
 }
@@ -1101,6 +1219,29 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook
     };
     for (size_t si = 0; si < plan.steps.size(); ++si) {
         const Step &s = plan.steps[si];
+        if (s.group >= 2 && (s.kind == S_GEMM || s.kind == S_DWPW)) {
+            // a launch group (group_siblings): one grid if the parts run the same grouped kernel
+            // instance at this batch, else the members one by one below
+            const int ng = std::min(s.group, ZR_GROUP_MAX);
+            GemmParams gp[ZR_GROUP_MAX];
+            DwPwParams dp[ZR_GROUP_MAX];
+            double bytes = 0, flops = 0;
+            for (int k = 0; k < ng; ++k) {
+                const Step &m = plan.steps[si + k];
+                if (s.kind == S_GEMM) gp[k] = gemm_of(m);
+                else dp[k] = dwpw_of(m);
+                bytes += m.bytes * b.N;
+                flops += m.flops * b.N;
+            }
+            if (hook) hook->before(stream);
+            const char *kname = s.kind == S_GEMM ? launch_gemm_group(gp, ng, stream) : launch_dwpw_group(dp, ng, stream);
+            if (kname) {
+                if (hook) hook->after(stream, kname, bytes, flops);
+                si += ng - 1;
+                continue;
+            }
+            if (hook) hook->cancel();
+        }
         Resolved out = resolve(s.out, plan, b);
         const char *kname = nullptr;
         if (hook) hook->before(stream);
@@ -1206,6 +1347,25 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook
             r.scale_y = s.scale_y;
             r.scale_x = s.scale_x;
             kname = launch_resize(r, stream);
+            break;
+        }
+        case S_DWGAP: {
+            DwParams d{};
+            d.in = plane_of(s.in, plan, b);
+            d.out = const_cast<float *>(out.p);
+            d.o_sN = out.sN;
+            d.o_sC = out.sC;
+            d.OH = s.dw_oh;
+            d.OW = s.dw_ow;
+            d.N = b.N;
+            d.k = s.kh;
+            d.stride = s.stride;
+            d.pad_t = s.pad_t;
+            d.pad_l = s.pad_l;
+            d.w = W + s.w_off;
+            d.bias = W + s.b_off;
+            d.act = act_of(s.pre, W);
+            kname = launch_dwgap(d, stream);
             break;
         }
         case S_GAP: {

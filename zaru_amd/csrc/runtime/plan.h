@@ -18,7 +18,9 @@
 
 namespace zr {
 
-enum StepKind { S_GEMM, S_DW, S_DIRECT, S_ELT, S_RESIZE, S_GAP, S_DWPW };
+// S_DWGAP: a depthwise conv (S_DW fields) whose only consumer was a global average pool; `out`
+// is the pooled vector
+enum StepKind { S_GEMM, S_DW, S_DIRECT, S_ELT, S_RESIZE, S_GAP, S_DWPW, S_DWGAP };
 
 struct TRef {
     int kind = 0;  // 0 internal storage, 1 graph input, 2 graph output
@@ -50,11 +52,16 @@ struct Step {
     // S_DWPW: the depthwise conv in front of the 1x1 (kh/kw/stride/pads above describe it)
     int64_t dw_w_off = -1, dw_b_off = -1;
     ActDesc dw_act;
+    // S_DWGAP: the depthwise output plane (pooled away)
+    int dw_oh = 0, dw_ow = 0;
     // S_DIRECT: runs as stem_kernel (Cin = 3, weights padded to 32 output channels)
     bool stem = false;
     // algorithmic traffic / work per image (for roofline accounting); bytes_pre: the same
     // step sampling its input from RGBA frames (4 B per input pixel instead of 12)
     double bytes = 0, flops = 0, bytes_pre = 0;
+    // launch grouping (group_siblings): the first step of a group of independent sibling steps
+    // holds the group's size (>= 2) and the members follow it; 1 = launched alone, 0 = a member
+    int group = 1;
 };
 
 struct PlanOutput {
@@ -101,6 +108,7 @@ struct LaunchHook {
     virtual ~LaunchHook() = default;
     virtual void before(hipStream_t s) = 0;
     virtual void after(hipStream_t s, const char *kernel, double bytes, double flops) = 0;
+    virtual void cancel() {}  // the launch announced by before() did not happen
 };
 
 void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook *hook = nullptr);

@@ -159,6 +159,10 @@ struct Profiler final : zr::LaunchHook {
         pending = get();
         (void)hipEventRecord(pending, s);
     }
+    void cancel() override {
+        if (pending) pool.push_back(pending);
+        pending = nullptr;
+    }
     void after(hipStream_t s, const char *k, double bytes, double flops) override {
         hipEvent_t e = get();
         (void)hipEventRecord(e, s);
@@ -393,7 +397,7 @@ int zr_plan_describe(const uint8_t *onnx, size_t len, const uint32_t *out_sel, s
         zr::Plan plan;
         std::vector<uint32_t> sel(out_sel, out_sel + n_sel);
         if (!zr::compile_plan(m, sel, plan, err)) return set_err(ZR_ERR_MODEL, err);
-        static const char *kinds[] = {"gemm", "dw", "direct", "elt", "resize", "gap", "dwpw"};
+        static const char *kinds[] = {"gemm", "dw", "direct", "elt", "resize", "gap", "dwpw", "dwgap"};
         static const char *acts[] = {"none", "relu", "clip", "prelu", "sigmoid"};
         std::string t;
         char line[512];
@@ -414,11 +418,11 @@ int zr_plan_describe(const uint8_t *onnx, size_t len, const uint32_t *out_sel, s
         }
         for (auto &st : plan.steps) {
             snprintf(line, sizeof line,
-                     "%s%s in=%s out=%s k=%dx%d s=%d M=%d K=%d KK=%d pre=%s post=%s res=%d rC=%d elt=%d off=%lld oN=%lld oC=%lld oP=%lld in2=%s\n",
+                     "%s%s in=%s out=%s k=%dx%d s=%d M=%d K=%d KK=%d pre=%s post=%s res=%d rC=%d elt=%d off=%lld oN=%lld oC=%lld oP=%lld in2=%s grp=%d\n",
                      kinds[st.kind], st.stem ? " stem" : "", ref(st.in).c_str(), ref(st.out).c_str(), st.kh, st.kw, st.stride,
                      st.M, st.K, st.KK, acts[st.pre.kind], acts[st.post.kind], st.res_mode, st.r_C,
                      st.elt_op, (long long)st.out.off, (long long)st.out.o_sN, (long long)st.out.o_sC,
-                     (long long)st.out.o_sP, (st.res_mode || st.kind == zr::S_ELT) ? ref(st.in2).c_str() : "-");
+                     (long long)st.out.o_sP, (st.res_mode || st.kind == zr::S_ELT) ? ref(st.in2).c_str() : "-", st.group);
             t += line;
         }
         if (needed) *needed = t.size() + 1;

@@ -66,4 +66,57 @@ struct JpegHuffParams {
 int jpeg_huff_max_lds();          // the most dynamic LDS one workgroup may stage
 const char *launch_jpeg_huff(const JpegHuffParams &p, hipStream_t s);
 
+// Self-synchronising entropy decoding (jpeg_sync.hip) for streams without restart intervals:
+// the unstuffed scan is cut into JS_SEG-bit segments, one lane each.  A lane first decodes its
+// segment from a guessed state (its first bit, first block of an MCU); Huffman decoders that
+// start out of step fall into step with the true one within a few symbols, so the exit state a
+// lane reaches (the first block boundary past its segment) is, almost always, the true state of
+// the next lane's start.  Sync passes re-decode each lane from its predecessor's exit until the
+// lane meets a checkpoint of its earlier decode (same bit, same block of the MCU: the same state,
+// so the rest is unchanged); then a scan over the lanes gives each one its first block index and
+// DC predictors, and a final pass writes the coefficients.
+constexpr int JS_SEG = 4096;  // bits per segment (a multiple of 128)
+constexpr int JS_CK = 8;      // checkpoints per segment: the first block boundary at or past each
+                              // JS_SEG / JS_CK-bit mark; the last one is the lane's exit
+constexpr int JS_LANES = 64;  // segments per workgroup
+constexpr int JS_MARGIN = 4096;  // bytes staged past a workgroup's last segment (blocks that run over)
+// bits a lane's guessed decode runs before its segment, to fall into step (per frame: about a
+// dozen blocks' worth of the frame's average, a multiple of 128)
+constexpr int JS_WARM_MIN = 2048, JS_WARM_MAX = 32768;
+struct JpegSyncState {
+    int32_t pos, u, nblk;       // bit, block of the MCU, blocks since the lane's start
+    int32_t err;                // first block since the start with a bad code / AC index, + 1 (0: none)
+    int32_t dc[3], pad;         // DC differences since the lane's start, per component
+};
+struct JpegSyncFrame {
+    const JpegHuffTable *tables;  // [8]
+    const uint8_t *data;          // the scan, unstuffed (16-B aligned, zero slack past the end)
+    int nbytes, nbits, nseg, nblocks, bpm, mcux, ncomp, warm;
+    int ucomp[10], uby[10], ubx[10];  // block u of an MCU: component, block row / column offset
+    int td[3], ta[3], ch[3], cv[3], bw[3];
+    int16_t *coef;
+    int64_t coef_off[3];
+    JpegSyncState *ck;            // [nseg][JS_CK]
+    JpegSyncState *x;             // [nseg] exit states
+    int2 *start;                  // [nseg] the (pos, u) the lane's checkpoints were decoded from
+    int32_t *base;                // [nseg] first block index (-1: nothing to write)
+    int32_t *pred;                // [nseg][3] DC predictors at the lane's start
+    int32_t *err_block;           // [1] blocks from here on are zero (nblocks: none)
+    int frame;                    // index into the call's error flags
+};
+struct JpegSyncParams {
+    const JpegSyncFrame *frames;
+    const int32_t *wg;            // [n_wg][2]: frame, first segment
+    int n_wg, nframes;
+    int *error;                   // [frame of the call]
+    int *changed;                 // [JS_PASSES + 1] exits changed per pass (zeroed per call)
+    int lds_bytes;                // dynamic LDS: the largest warm-up + 64 segments + margin of the call
+};
+constexpr int JS_PASSES = 32;     // sync passes launched per call at most (each returns at once
+                                  // once a pass changed nothing)
+constexpr int JS_MAX_BITS_PER_BLOCK = 600;  // denser scans decode on the host
+// pass 0: the guessed decode, 1..JS_PASSES: sync passes; then prefix, write and zero fill
+const char *launch_jpeg_sync_scan(const JpegSyncParams &p, int pass, hipStream_t s);
+const char *launch_jpeg_sync_finish(const JpegSyncParams &p, hipStream_t s);
+
 }  // namespace zr

@@ -188,7 +188,9 @@ struct DwPwParams {
 //   vres: VALU dwpw taking the block's residual from the staged depthwise taps
 //   vstore: 16-B row-segment GEMM epilogue
 //   ws: warp-specialized persistent MFMA dwpw (dwpw_ws.hip)
-enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_VRES, FORM_VSTORE, FORM_WS, FORM_COUNT };
+//   groups: sibling steps launched as one grid (plan.cpp group_siblings, kernels/group.h)
+//   dwgap: depthwise + global average pool in one launch (plan.cpp fuse_dw_gap)
+enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_VRES, FORM_VSTORE, FORM_WS, FORM_GROUPS, FORM_DWGAP, FORM_COUNT };
 bool form_on(Form f);
 
 bool stem_supported(int cin, int k, int stride, int cout);
@@ -206,11 +208,20 @@ const char *launch_direct(const DirectParams &p, hipStream_t s);
 const char *launch_elt(const EltParams &p, hipStream_t s);
 const char *launch_resize(const ResizeParams &p, hipStream_t s);
 const char *launch_gap(const GapParams &p, hipStream_t s);
+// depthwise + activation + global average pool in one launch (out / o_sN / o_sC: the pooled
+// vector); planes of <= 512 floats (64 of them staged in LDS)
+const char *launch_dwgap(const DwParams &p, hipStream_t s);
 const char *launch_preproc(const PreprocParams &p, hipStream_t s);
 const char *launch_candidates(const CandParams &p, hipStream_t s);
 const char *launch_stem(const StemParams &p, bool pre, hipStream_t s);
 const char *launch_dwpw(const DwPwParams &p, hipStream_t s);
 const char *launch_dwpw_mfma(const DwPwParams &p, hipStream_t s);  // the MFMA forms (dwpw_mfma.hip)
-const char *launch_dwpw_ws(const DwPwParams &p, hipStream_t s);    // nullptr: the layer does not fit it
+const char *launch_dwpw_ws(const DwPwParams &p, hipStream_t s, bool launch);  // nullptr: the layer does not fit it
+constexpr int ZR_GROUP_MAX = 4;  // steps per launch group
+// Sibling steps (independent, same kernel instance) in one launch (kernels/group.h); nullptr
+// when the parts would not run the same grouped instance: the caller launches them one by one.
+const char *launch_gemm_group(const GemmParams *p, int n, hipStream_t s);
+const char *launch_dwpw_group(const DwPwParams *p, int n, hipStream_t s);
+const char *launch_dwpw_mfma_group(const DwPwParams *p, int n, hipStream_t s);
 
 }  // namespace zr
