@@ -823,7 +823,13 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
             F.nblocks = nmcu[f] * u;
             // warm-up: ~12 average blocks (high-rate scans fall into step over more bits)
             const int64_t bpb = (int64_t)F.nbits / std::max(1, F.nblocks);
-            F.warm = (int)std::min<int64_t>(zr::JS_WARM_MAX, std::max<int64_t>(zr::JS_WARM_MIN, (12 * bpb + 127) / 128 * 128));
+            static const int warm_blocks = [] {  // ZARU_JPEG_SYNC_WARM: warm-up in average blocks (A/B)
+                const char *e = std::getenv("ZARU_JPEG_SYNC_WARM");
+                const long v = e ? std::strtol(e, nullptr, 10) : 0;
+                return v > 0 ? (int)v : 12;
+            }();
+            F.warm = (int)std::min<int64_t>(zr::JS_WARM_MAX,
+                                            std::max<int64_t>(zr::JS_WARM_MIN, (warm_blocks * bpb + 127) / 128 * 128));
             sync_lds = std::max(sync_lds, F.warm / 8 + zr::JS_LANES * (zr::JS_SEG / 8) + zr::JS_MARGIN);
             F.coef = dec->d_coef + cofs[f] * 64;
             F.frame = (int)f;
