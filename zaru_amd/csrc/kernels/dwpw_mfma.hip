@@ -497,9 +497,9 @@ static int dfkc_env() {
 // 6^2 / 3^2 blocks at 341 images: half the dependent DMA round trips of a workgroup that is
 // alone on its CU, 18.9 -> 17.0 us at 3^2, profiles/r04_layers/), else 16 (at 12^2 and up the
 // wider chunk's DMA costs more than the barriers it saves: r03).  ZARU_HIP_DFKC forces one.
-static int dfkc_for(int wgs) {
+static int dfkc_for(int wgs, int cin) {
     if (const int e = dfkc_env()) return e;
-    return wgs < 512 ? 32 : 16;
+    return wgs < 512 && cin >= 64 ? 32 : 16;  // (32 channels in one chunk measured slower: 12.9 -> 15.2 us)
 }
 
 template <int K, int S, int WM, int MTW>
@@ -512,7 +512,7 @@ const char *dwpw_go(const DwPwParams &p, hipStream_t s) {
     if constexpr (K == 3 && MTW == 1) {
         // wider channel chunks: fewer dependent DMA round trips per tile (the 6^2 / 3^2 launches
         // of a few dozen workgroups are nothing but those round trips)
-        const int dk = dfkc_for(nct * mb);
+        const int dk = dfkc_for(nct * mb, p.g.K);
         if (dk >= 64)
             if (const size_t lds = dma_plan<K, S, WM, MTW, 64>(p, &runmax, &bufsz)) {
                 hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, 64>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
@@ -658,7 +658,7 @@ const char *launch_dwpw_mfma_group(const DwPwParams *p, int n, hipStream_t s) {
     const int bn = (4 / l0->wm) * 32;
     int wgs = 0;
     for (int i = 0; i < n; ++i) wgs = std::max(wgs, (p[i].g.ncols + bn - 1) / bn);
-    const int dk = dfkc_for(wgs);
+    const int dk = dfkc_for(wgs, p[0].g.K);
     if (dk == 32) return p[0].stride == 1 ? dma_group_layout<3, 1, 32>(p, n, *l0, s) : dma_group_layout<3, 2, 32>(p, n, *l0, s);
     if (dk == 16) return p[0].stride == 1 ? dma_group_layout<3, 1, 16>(p, n, *l0, s) : dma_group_layout<3, 2, 16>(p, n, *l0, s);
     return nullptr;

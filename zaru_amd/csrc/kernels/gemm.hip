@@ -310,86 +310,95 @@ void gemm_tiled_group_kernel(const LaunchGroup<GemmParams> G) {
 // plane, M = 1404 / 1, K = Cin * 9) with the images as the GEMM's rows: C^T[n][m] =
 // X^T[n][k] . W^T[k][m].  The column-per-image form reads X with a stride of one image per lane
 // and stores each output row with a stride of M per lane; here a lane's B fragment
-// W^T[k][m0 + lane % 32] and its stores out[n][m0 + lane % 32] are coalesced 128-B rows, and
-// the A fragment X^T[n0 + lane % 32][k] stays L1/L2-resident (the 4 waves of a workgroup share
-// it: 32 images x 4 M-tiles).  The next 32-deep K-chunk's fragments are loaded while the
-// current chunk's 16 MFMAs run.
+// W^T[k][m0 + lane % 16] and its stores out[n][m0 + lane % 16] are coalesced rows, and the A
+// fragment X^T[n0 + lane % 16][k] stays L1/L2-resident.  16x16 tiles of v_mfma_f32_16x16x4_f32:
+// each wave's chain is K / 4 MFMAs of 8 passes (the 32x32x2 form: K / 2 of 16 passes, 4x the
+// chain latency for these 1-output-position launches), and a launch has 4x the waves.  The
+// 16x16x4 MFMA sums each output's products in k order exactly as the 32x32x2 one and an fmaf
+// chain do (tools/debug/mfma_order.hip, profiles/r04_mfma_order_probe.json), so the bits are
+// the other forms' (tests/test_gpu_forms.py switches this one off).
 // NCH > 0: the K loop fully unrolled for exactly NCH 32-deep chunks (the FaceMesh heads: K = 288,
-// 9 chunks).  The runtime loop's back edge makes the compiler's wait counting drain every load
-// (vmcnt(0)) before each chunk's MFMAs, prefetched chunk included; straight-line code keeps the
-// next chunk's loads in flight.  Same k order, same bits.
+// 9 chunks): straight-line code keeps the next chunk's loads in flight (a runtime loop's back
+// edge makes the compiler's wait counting drain them).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int RC = 32;  // K per chunk (8 MFMA steps of 4)
+
 template <bool FULLPLANE, int NCH>
 __device__ __forceinline__ void gemm_rows_body(const GemmParams &P, int mtiles, int bx, int by) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int kh = lane >> 5, col = lane & 31;
+    const int r = lane & 15, kq = lane >> 4;
     const int mt = by * 4 + wave;
     if (mt >= mtiles) return;  // no barriers in this kernel
-    const int m0 = mt * 32, n0 = bx * 32;
+    const int m0 = mt * 16, n0 = bx * 16;
     const int nimg = P.ncols;  // P == 1: one column per image
-    const int na = min(n0 + col, nimg - 1);
+    const int na = min(n0 + r, nimg - 1);
     const float *xa = P.x + (int64_t)na * P.x_sN;
-    const float *wb = P.wt + m0 + col;  // [Kpad][Mpad]
+    const float *wb = P.wt + m0 + r;  // [Kpad][Mpad]
 
-    float a[2][KC / 2], b[2][KC / 2];
-    // k = ci * KK + kq of this lane's next A element, advanced by 2 per k-step (KK >= 2: at most
-    // one wrap), so no per-element integer division
-    int ci = 0, kq = kh;
+    float a[2][RC / 4], b[2][RC / 4];
+    // k = ci * KK + kk of this lane's next A element, advanced by 4 per step (no division)
+    int ci = 0, kk = kq;
+    if constexpr (FULLPLANE) {
+        while (kk >= P.KK) {
+            kk -= P.KK;
+            ++ci;
+        }
+    }
     auto load = [&](int kc, int buf) {
 #pragma unroll
-        for (int s = 0; s < KC / 2; ++s) {
-            const int k = kc + 2 * s + kh;
+        for (int t = 0; t < RC / 4; ++t) {
+            const int k = kc + 4 * t + kq;
             float v;
             if constexpr (FULLPLANE) {
                 const bool in = k < P.K;
-                v = xa[in ? (uint32_t)ci * (uint32_t)P.x_sC + (uint32_t)kq * (uint32_t)P.x_sK : 0u];
-                kq += 2;
-                const bool wrap = kq >= P.KK;
-                kq -= wrap ? P.KK : 0;
-                ci += wrap ? 1 : 0;
+                v = xa[in ? (uint32_t)ci * (uint32_t)P.x_sC + (uint32_t)kk * (uint32_t)P.x_sK : 0u];
+                kk += 4;
+                while (kk >= P.KK) {
+                    kk -= P.KK;
+                    ++ci;
+                }
             } else {
                 v = xa[(int64_t)(k < P.K ? k : P.K - 1) * P.x_sC];
             }
-            a[buf][s] = k < P.K ? v : 0.f;
-            b[buf][s] = wb[(int64_t)(k < P.Kpad ? k : 0) * P.Mpad];
-            if (k >= P.Kpad) b[buf][s] = 0.f;
+            a[buf][t] = k < P.K ? v : 0.f;
+            b[buf][t] = wb[(int64_t)(k < P.Kpad ? k : 0) * P.Mpad];
+            if (k >= P.Kpad) b[buf][t] = 0.f;
         }
     };
-    f32x16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     load(0, 0);
     if constexpr (NCH > 0) {
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
-            if (c + 1 < NCH) load((c + 1) * KC, (c + 1) & 1);
+            if (c + 1 < NCH) load((c + 1) * RC, (c + 1) & 1);
 #pragma unroll
-            for (int s = 0; s < KC / 2; ++s)
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c & 1][s], b[c & 1][s], acc, 0, 0, 0);
+            for (int t = 0; t < RC / 4; ++t)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c & 1][t], b[c & 1][t], acc, 0, 0, 0);
         }
-    } else for (int kc = 0; kc < P.Kpad; kc += 2 * KC) {
-        if (kc + KC < P.Kpad) load(kc + KC, 1);
+    } else for (int kc = 0; kc < P.Kpad; kc += 2 * RC) {
+        if (kc + RC < P.Kpad) load(kc + RC, 1);
 #pragma unroll
-        for (int s = 0; s < KC / 2; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][s], b[0][s], acc, 0, 0, 0);
-        if (kc + KC >= P.Kpad) break;
-        if (kc + 2 * KC < P.Kpad) load(kc + 2 * KC, 0);
+        for (int t = 0; t < RC / 4; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][t], b[0][t], acc, 0, 0, 0);
+        if (kc + RC >= P.Kpad) break;
+        if (kc + 2 * RC < P.Kpad) load(kc + 2 * RC, 0);
 #pragma unroll
-        for (int s = 0; s < KC / 2; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][s], b[1][s], acc, 0, 0, 0);
+        for (int t = 0; t < RC / 4; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1][t], b[1][t], acc, 0, 0, 0);
     }
 
-    // acc[r] = C^T[n0 + mfma32_row(r, kh)][m0 + col]
-    const int m = m0 + col;
+    // acc[i] = C^T[n0 + 4 * kq + i][m0 + r]
+    const int m = m0 + r;
     if (m >= P.M) return;
     const float bias = P.bias[m];
-    float v[16];
+    float v[4];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = acc[r] + bias;
+    for (int i = 0; i < 4; ++i) v[i] = acc[i] + bias;
     auto chan = [&](int) { return m; };
-    apply_act_n<16>(P.pre, v, chan);
-    apply_act_n<16>(P.post, v, chan);
+    apply_act_n<4>(P.pre, v, chan);
+    apply_act_n<4>(P.post, v, chan);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int n = n0 + mfma32_row(r, kh);
-        if (n < nimg) P.out[(uint32_t)n * (uint32_t)P.o_sN + (uint32_t)m * (uint32_t)P.o_sC] = v[r];
+    for (int i = 0; i < 4; ++i) {
+        const int n = n0 + 4 * kq + i;
+        if (n < nimg) P.out[(uint32_t)n * (uint32_t)P.o_sN + (uint32_t)m * (uint32_t)P.o_sC] = v[i];
     }
 }
 
@@ -445,9 +454,10 @@ static GemmChoice choose_gemm(const GemmParams &p) {
     }
     if (p.P == 1 && p.res_mode == 0 && p.KK > 1 && form_on(FORM_ROWS)) {  // a head over whole planes (KK >= 2)
         c.form = GF_ROWS;
-        c.v0 = (p.Kpad + KC - 1) / KC == 9 ? 9 : 0;
-        c.gx = (p.ncols + 31) / 32, c.gy = (mtiles + 3) / 4;
-        c.a0 = mtiles;
+        c.v0 = (p.Kpad + RC - 1) / RC == 9 ? 9 : 0;
+        const int mt16 = (p.Mpad + 15) / 16;  // 16-row tiles
+        c.gx = (p.ncols + 15) / 16, c.gy = (mt16 + 3) / 4;
+        c.a0 = mt16;
         return c;
     }
     const int bx = (p.ncols + 127) / 128;
