@@ -446,7 +446,10 @@ def main():
     if world > 1:
         # one node: the RCCL bootstrap needs no network interface beyond loopback
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
-        dist.init_process_group("gloo")  # control plane only (ids, barriers, max / sum)
+        from zaru_amd._lib import _StdoutToStderr
+        with _StdoutToStderr():  # gloo's connection notices: stdout carries the one JSON line
+            dist.init_process_group("gloo")  # control plane only (ids, barriers, max / sum)
+            dist.barrier()
 
     import zaru_amd.host as H
     from zaru_amd import shard

@@ -178,6 +178,23 @@ def synchronize(stream=None):
     check(lib().zr_stream_synchronize(stream))
 
 
+class _StdoutToStderr:
+    """RCCL prints a version banner on stdout when it initialises; bench.py's one JSON line on
+    stdout must stay the only thing there, so fd 1 points at stderr meanwhile."""
+
+    def __enter__(self):
+        import os
+        import sys
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        import os
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 class Comm:
     """The node communicator of the multi-GPU path (zr_comm_*): RCCL over xGMI,
     one rank per GPU.  `unique_id()` on one rank; its 128 bytes reach the others by any side
@@ -186,7 +203,8 @@ class Comm:
     @staticmethod
     def unique_id() -> bytes:
         buf = (C.c_uint8 * 128)()
-        check(lib().zr_comm_unique_id(buf))
+        with _StdoutToStderr():
+            check(lib().zr_comm_unique_id(buf))
         return bytes(buf)
 
     def __init__(self, uid: bytes, world: int, rank: int, device: int):
@@ -194,7 +212,8 @@ class Comm:
             raise ValueError("a communicator id is 128 bytes")
         p = C.c_void_p()
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
-        check(lib().zr_comm_create(buf, world, rank, device, C.byref(p)))
+        with _StdoutToStderr():
+            check(lib().zr_comm_create(buf, world, rank, device, C.byref(p)))
         self.ptr, self.world, self.rank = p.value, world, rank
 
     def all_gather_async(self, d_send: int, d_recv: int, nbytes: int, stream=None):
