@@ -254,8 +254,12 @@ int zr_jpeg_decode_async(zr_jpeg_decoder *d, const uint8_t *jpeg, size_t len, ui
                          size_t row_stride, void *hip_stream);
 /* n frames (<= 4096) in one call: frame i from jpegs[i] (lens[i] bytes) into d_rgba[i].  Every
  * frame is parsed before anything is enqueued (an error names the frame); the device-decodable
- * frames share one Huffman launch, so a multi-camera ingest fills the GPU with one call instead
- * of one small launch per frame.  zr_jpeg_decode_async is the n = 1 case. */
+ * frames share one set of Huffman launches, so a multi-camera ingest fills the GPU with one call
+ * instead of one small launch per frame.  zr_jpeg_decode_async is the n = 1 case.  Huffman
+ * decoding runs on the device for streams with restart intervals (one lane per interval) and
+ * for streams without them (self-synchronising decoding, one lane per 4096-bit segment, round 4)
+ * unless their scan averages > 600 bits per block (near-lossless noise: those sync too slowly)
+ * or ZARU_JPEG_SYNC=0; the rest, and every frame under ZARU_JPEG_HOST_ENTROPY=1, on the host. */
 int zr_jpeg_decode_batch_async(zr_jpeg_decoder *d, size_t n, const uint8_t *const *jpegs, const size_t *lens,
                                uint8_t *const *d_rgba, const size_t *row_strides, void *hip_stream);
 /* Host-only half (no GPU): the frame's block layout and, when `coef` is given, its quantised
@@ -269,8 +273,9 @@ typedef struct {
  * NULL; waits for the last call) is 1 when a frame of the LAST call held an invalid Huffman code or
  * AC index.  Error contract: a frame decoded on the host with corrupt data fails the call
  * (ZR_ERR_INVALID_ARGUMENT, frame named); on the device it cannot fail the already-returned call,
- * so the rest of the corrupt interval decodes as all-zero blocks (libjpeg-turbo's insufficient-
- * data behaviour) and the frame's flag is set -- zr_jpeg_frame_errors names the frames. */
+ * so the rest of the corrupt interval (a stream without restart intervals: every block from the
+ * bad one to the end of the frame) decodes as all-zero blocks (libjpeg-turbo's insufficient-data
+ * behaviour) and the frame's flag is set -- zr_jpeg_frame_errors names the frames. */
 int zr_jpeg_decoder_status(zr_jpeg_decoder *d, uint64_t *gpu_entropy, uint64_t *host_entropy, int *corrupt);
 /* per frame of the last call: 1 = corrupt entropy data (waits for that call); *n = its frame count */
 int zr_jpeg_frame_errors(zr_jpeg_decoder *d, int32_t *flags, size_t cap, size_t *n);

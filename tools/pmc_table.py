@@ -14,7 +14,7 @@ CLK_GHZ, SIMDS = 2.4, 1024
 
 
 def sym(name):
-    name = name.split("(")[0]
+    name = name.replace("(anonymous namespace)::", "").split("(")[0]
     return (name.split("zr::", 1)[-1] if "zr::" in name else name.split(" ")[-1]).replace(" ", "")
 
 
