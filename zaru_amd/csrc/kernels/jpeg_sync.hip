@@ -16,12 +16,7 @@ using namespace jpegbits;
 
 constexpr int JS_CKB = JS_SEG / JS_CK;  // bits between checkpoint marks
 
-// first staged bit of the workgroup whose first segment is s0 (its first lane's warm-up included)
-__device__ __forceinline__ int stage_bit(const JpegSyncFrame &F, int s0) { return s0 > 0 ? s0 * JS_SEG - F.warm : 0; }
-// bytes a workgroup stages: the warm-up, its 64 segments and the overrun margin
-__device__ __forceinline__ int stage_bytes(const JpegSyncFrame &F) { return F.warm / 8 + JS_LANES * (JS_SEG / 8) + JS_MARGIN; }
-
-// One block at bit `bp` (relative to the staged range): the DC difference, the AC coefficients
+// One block at bit `bp`: the DC difference, the AC coefficients
 // into `co` (natural order, WRITE only), false on a bad code / AC index (T.81 F.2.2: the block is
 // not decoded further).
 template <bool WRITE>
@@ -69,24 +64,25 @@ __device__ __forceinline__ void publish(const JpegSyncParams &P, int pass, JpegS
     }
 }
 
-// The workgroup's tables and scan range in LDS (big-endian dwords): bytes [a0, a0 + n16 * 16)
-// of the frame's data, which the host pads with zeros to cover every workgroup's range.
-__device__ __forceinline__ void stage(const JpegSyncFrame &F, int s0, JpegHuffTable *T, uint4 *sdata) {
+// The frame's 8 tables into the workgroup's LDS.  The scan itself is read from global memory
+// (L1 / L2; a lane's window loads the dword two ahead of its position, so the load is off the
+// symbol chain): staging a workgroup's bit range in LDS held the kernel to one 64-lane workgroup
+// (< 1 wave per SIMD) per 56 KB, and these lanes are latency-bound -- occupancy is what pays.
+__device__ __forceinline__ void stage_tables(const JpegSyncFrame &F, JpegHuffTable *T) {
     const uint4 *src = reinterpret_cast<const uint4 *>(F.tables);
     uint4 *dst = reinterpret_cast<uint4 *>(T);
     constexpr int n16 = (int)(8 * sizeof(JpegHuffTable) / 16);
-    for (int i = threadIdx.x; i < n16; i += 64) dst[i] = src[i];
-    const uint4 *d = reinterpret_cast<const uint4 *>(F.data + (size_t)stage_bit(F, s0) / 8);
-    const int n16d = stage_bytes(F) / 16;
-    for (int i = threadIdx.x; i < n16d; i += 256) {
-        uint4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-            if (i + 64 * u < n16d) v[u] = d[i + 64 * u];
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-            if (i + 64 * u < n16d)
-                sdata[i + 64 * u] = make_uint4(bswap32(v[u].x), bswap32(v[u].y), bswap32(v[u].z), bswap32(v[u].w));
+    for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+}
+
+// The unstuffed scan as big-endian dwords (what the bit window reads), per frame.
+__global__ __launch_bounds__(256) void jpeg_sync_bswap_kernel(const JpegSyncParams P) {
+    const JpegSyncFrame &F = P.frames[blockIdx.y];
+    const uint4 *src = reinterpret_cast<const uint4 *>(F.data);
+    uint4 *dst = reinterpret_cast<uint4 *>(F.words);
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < F.nwords / 4; i += gridDim.x * 256) {
+        const uint4 v = src[i];
+        dst[i] = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
     }
 }
 
@@ -97,9 +93,8 @@ __device__ __forceinline__ void stage(const JpegSyncFrame &F, int s0, JpegHuffTa
 // (or a half-written one) only gets ahead (or is redone next pass); a pass runs only while the
 // previous one changed an exit, and the prefix pass checks every start against its predecessor's
 // final exit.
-__global__ __launch_bounds__(64) void jpeg_sync_scan_kernel(const JpegSyncParams P, int pass) {
+__global__ __launch_bounds__(256) void jpeg_sync_scan_kernel(const JpegSyncParams P, int pass) {
     __shared__ JpegHuffTable T[8];
-    extern __shared__ uint4 sdata[];
     if (pass > 0 && __atomic_load_n(&P.changed[pass - 1], __ATOMIC_RELAXED) == 0) return;  // converged
     if (pass == 0 && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&P.changed[0], 1);
     const JpegSyncFrame &F = P.frames[P.wg[2 * blockIdx.x]];
@@ -126,18 +121,18 @@ __global__ __launch_bounds__(64) void jpeg_sync_scan_kernel(const JpegSyncParams
     } else if (work) {
         // the guess: the first block of an MCU, JS_WARM bits before the segment (lane 0: the
         // scan's true start); the lane's own start is its first block boundary in its segment
-        st.pos = s > 0 ? s * JS_SEG - F.warm : 0;
+        st.pos = max(0, s * JS_SEG - F.warm);
         F.start[s] = make_int2(-1, -1);  // (set when the decode reaches the segment)
     }
     if (!__syncthreads_or(work)) return;
-    stage(F, s0, T, sdata);
+    stage_tables(F, T);
     __syncthreads();
     if (!work) return;
 
-    const int a0b = stage_bit(F, s0);  // first staged bit
+    const int a0b = 0;  // (bit positions are the scan's own)
     Window win;
-    win.init(reinterpret_cast<const uint32_t *>(sdata), stage_bytes(F) / 4 - 1, st.pos - a0b, F.nbits - a0b);
-    const int lim = stage_bytes(F) * 8 - 64 + a0b;  // positions past the staged range: an error
+    win.init(F.words, F.nwords - 1, st.pos, F.nbits);
+    const int lim = F.nwords * 32 - 64;  // positions past the padded scan: an error
     const int seg_lo = s * JS_SEG;
     JpegSyncState *const ck = F.ck + (size_t)s * JS_CK;
     int bp = st.pos - a0b;
@@ -287,27 +282,25 @@ __global__ __launch_bounds__(256) void jpeg_sync_prefix_kernel(const JpegSyncPar
 }
 
 // The write pass: every live lane decodes its blocks from its start into the coefficient array.
-__global__ __launch_bounds__(64) void jpeg_sync_write_kernel(const JpegSyncParams P) {
+__global__ __launch_bounds__(256) void jpeg_sync_write_kernel(const JpegSyncParams P) {
     __shared__ JpegHuffTable T[8];
     __shared__ uint8_t zz[64];
-    __shared__ int4 sblk[64][8];
-    extern __shared__ uint4 sdata[];
+    __shared__ int4 sblk[256][8];
     const JpegSyncFrame &F = P.frames[P.wg[2 * blockIdx.x]];
     const int s0 = P.wg[2 * blockIdx.x + 1];
     const int s = s0 + (int)threadIdx.x;
     const int base = s < F.nseg ? F.base[s] : -1;
     if (!__syncthreads_or(base >= 0)) return;
-    stage(F, s0, T, sdata);
-    zz[threadIdx.x] = kZigzag[threadIdx.x];
+    stage_tables(F, T);
+    if (threadIdx.x < 64) zz[threadIdx.x] = kZigzag[threadIdx.x];
     __syncthreads();
     if (base < 0) return;
     const JpegSyncState e = F.x[s];
     const int2 st = F.start[s];
     const int end = min(base + e.nblk, F.err_block[0]);
-    const int a0b = stage_bit(F, s0);
     Window win;
-    win.init(reinterpret_cast<const uint32_t *>(sdata), stage_bytes(F) / 4 - 1, st.x - a0b, F.nbits - a0b);
-    int bp = st.x - a0b;
+    win.init(F.words, F.nwords - 1, st.x, F.nbits);
+    int bp = st.x;
     int pred[3] = {F.pred[3 * s], F.pred[3 * s + 1], F.pred[3 * s + 2]};
     int4 *const mine = sblk[threadIdx.x];
     int16_t *const co = reinterpret_cast<int16_t *>(mine);
@@ -347,24 +340,17 @@ __global__ __launch_bounds__(256) void jpeg_sync_zero_kernel(const JpegSyncParam
     }
 }
 
-int sync_max_lds() { return JS_LANES * (JS_SEG / 8) + JS_WARM_MAX / 8 + JS_MARGIN; }
-
 }  // namespace
 
 const char *launch_jpeg_sync_scan(const JpegSyncParams &p, int pass, hipStream_t s) {
-    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(jpeg_sync_scan_kernel),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, sync_max_lds()) == hipSuccess;
-    (void)attr;
-    hipLaunchKernelGGL(jpeg_sync_scan_kernel, dim3(p.n_wg), dim3(64), (size_t)p.lds_bytes, s, p, pass);
+    if (pass == 0) hipLaunchKernelGGL(jpeg_sync_bswap_kernel, dim3(64, p.nframes), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(jpeg_sync_scan_kernel, dim3(p.n_wg), dim3(JS_LANES), 0, s, p, pass);
     return "jpeg_sync_scan_kernel";
 }
 
 const char *launch_jpeg_sync_finish(const JpegSyncParams &p, hipStream_t s) {
-    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(jpeg_sync_write_kernel),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, sync_max_lds()) == hipSuccess;
-    (void)attr;
     hipLaunchKernelGGL(jpeg_sync_prefix_kernel, dim3(p.nframes), dim3(256), 0, s, p);
-    hipLaunchKernelGGL(jpeg_sync_write_kernel, dim3(p.n_wg), dim3(64), (size_t)p.lds_bytes, s, p);
+    hipLaunchKernelGGL(jpeg_sync_write_kernel, dim3(p.n_wg), dim3(JS_LANES), 0, s, p);
     hipLaunchKernelGGL(jpeg_sync_zero_kernel, dim3(p.nframes), dim3(256), 0, s, p);
     return "jpeg_sync_write_kernel";
 }

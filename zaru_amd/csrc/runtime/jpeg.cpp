@@ -667,7 +667,8 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
         for (size_t f = 0; f < n; f++)
             if (sync[f]) {
                 const size_t nseg = (spad[f] - zr::JS_MARGIN - zr::JS_WARM_MAX / 8 - 16) / (zr::JS_SEG / 8);
-                sync_bytes += nseg * (zr::JS_CK * sizeof(zr::JpegSyncState) + sizeof(zr::JpegSyncState) + 8 + 4 + 12) + 16;
+                sync_bytes += nseg * (zr::JS_CK * sizeof(zr::JpegSyncState) + sizeof(zr::JpegSyncState) + 8 + 4 + 12) + 16 +
+                              (spad[f] + 15) / 16 * 16;  // (+ the big-endian copy of the scan)
             }
         if (sync_bytes) sync_bytes += 256;  // the per-pass change counters
         const bool grow = (size_t)blocks > dec->coef_cap || (size_t)pbytes > dec->planes_cap ||
@@ -846,6 +847,9 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
             sp += (size_t)nseg * 12;
             F.err_block = reinterpret_cast<int32_t *>(sp);
             sp += 16;
+            F.words = reinterpret_cast<uint32_t *>(sp);
+            F.nwords = (int)(spad[f] / 16 * 4);
+            sp += (spad[f] + 15) / 16 * 16;
             sy = (size_t)(sp - dec->d_sync);
             for (int g0 = 0; g0 < nseg; g0 += zr::JS_LANES) {
                 swg[2 * n_swg] = (int32_t)ns;

@@ -78,7 +78,7 @@ const char *launch_jpeg_huff(const JpegHuffParams &p, hipStream_t s);
 constexpr int JS_SEG = 4096;  // bits per segment (a multiple of 128)
 constexpr int JS_CK = 8;      // checkpoints per segment: the first block boundary at or past each
                               // JS_SEG / JS_CK-bit mark; the last one is the lane's exit
-constexpr int JS_LANES = 64;  // segments per workgroup
+constexpr int JS_LANES = 256;  // segments per workgroup (a lane each)
 constexpr int JS_MARGIN = 4096;  // bytes staged past a workgroup's last segment (blocks that run over)
 // bits a lane's guessed decode runs before its segment, to fall into step (per frame: about a
 // dozen blocks' worth of the frame's average, a multiple of 128)
@@ -91,6 +91,8 @@ struct JpegSyncState {
 struct JpegSyncFrame {
     const JpegHuffTable *tables;  // [8]
     const uint8_t *data;          // the scan, unstuffed (16-B aligned, zero slack past the end)
+    uint32_t *words;              // the same as big-endian dwords (jpeg_sync_bswap_kernel)
+    int nwords;                   // dwords of `data` incl. the slack (a multiple of 4)
     int nbytes, nbits, nseg, nblocks, bpm, mcux, ncomp, warm;
     int ucomp[10], uby[10], ubx[10];  // block u of an MCU: component, block row / column offset
     int td[3], ta[3], ch[3], cv[3], bw[3];
