@@ -68,7 +68,7 @@ CASES = [
     (1080, 1920, 90, 2, {"restart_marker_blocks": 4}),
     (1080, 1920, 75, 0, {"restart_marker_blocks": 7}),
     (720, 1280, 95, 1, {"restart_marker_blocks": 2}),
-    # long intervals (a 64-interval range over the LDS budget): host entropy decoding
+    # long intervals (one MCU row each: 68 lanes per frame)
     (1080, 1920, 90, 2, {"restart_marker_rows": 1}),
     (720, 1280, 95, 1, {"restart_marker_rows": 2}),
 ]
@@ -169,9 +169,9 @@ def test_truncated_scan_is_decoded_or_rejected(dec):
 
 def test_restart_streams_decode_on_the_device(dec):
     """Streams with >= 8 restart intervals short enough for a workgroup's LDS are entropy-decoded
-    on the GPU (decoder status), with no corrupt interval flagged; so are streams without DRI
-    (self-synchronising decoder, jpeg_sync.hip); restart streams whose intervals are too long stay
-    on the host path."""
+    on the GPU (decoder status), with no corrupt interval flagged -- long ones (one MCU row per
+    interval) too, since round 4 reads the intervals from global memory instead of staging them in
+    LDS -- and so are streams without DRI (self-synchronising decoder, jpeg_sync.hip)."""
     from zaru_amd.jpeg import JpegDecoder
     d = JpegDecoder(0)
     try:
@@ -183,7 +183,7 @@ def test_restart_streams_decode_on_the_device(dec):
         for data in (with_rst, long_rst, plain, gray_rst):
             assert np.array_equal(d.decode(data), libjpeg_turbo_rgba(data))
         gpu, host, corrupt = d.status()
-        assert (gpu, host, corrupt) == (3, 1, 0)
+        assert (gpu, host, corrupt) == (4, 0, 0)
     finally:
         d.close()
 
@@ -298,7 +298,7 @@ def test_restart_stream_cut_mid_scan(dec):
 def test_batch_decode_mixed_frames(dec):
     """zr_jpeg_decode_batch_async: frames of different sizes, subsamplings and entropy paths
     (restart intervals -> one shared device Huffman launch; no DRI -> the self-synchronising
-    device decoder; long intervals -> host) in one call, each equal to libjpeg-turbo's decode."""
+    device decoder) in one call, each equal to libjpeg-turbo's decode."""
     from zaru_amd._lib import DeviceBuffer, lib
     from zaru_amd.jpeg import JpegDecoder
     specs = [((1080, 1920), 90, 2, {"restart_marker_blocks": 4}),
@@ -318,7 +318,7 @@ def test_batch_decode_mixed_frames(dec):
         lib().zr_stream_synchronize(None)
         for i, (data, (h, w)) in enumerate(zip(datas, shapes)):
             assert np.array_equal(bufs[i].download((h, w, 4), "uint8"), libjpeg_turbo_rgba(data)), i
-        assert d.status() == (6, 1, 0)
+        assert d.status() == (7, 0, 0)
     finally:
         d.close()
 

@@ -15,42 +15,29 @@ using namespace jpegbits;
 
 
 // Every coefficient goes to the lane's block in LDS (natural order through an LDS zig-zag table)
-// and the finished block leaves in eight 16-B stores.
-__global__ __launch_bounds__(64) void jpeg_huff_kernel(const JpegHuffParams P) {
+// and the finished block leaves in eight 16-B stores.  The interval bits are read from global
+// memory (the call's big-endian copy; the window's look-ahead load is off the symbol chain): a
+// workgroup of 256 lanes then needs 19 KB of tables + 32 KB of blocks in LDS, 3 workgroups per
+// CU, where staging each 64-interval range in LDS held the kernel to about one wave per CU.
+__global__ __launch_bounds__(JH_LANES) void jpeg_huff_kernel(const JpegHuffParams P) {
     __shared__ JpegHuffTable T[8];
     __shared__ uint8_t zz[64];
-    __shared__ int4 sblk[64][8];  // one 64-coefficient int16 block per lane
-    extern __shared__ uint4 sdata[];
+    __shared__ int4 sblk[JH_LANES][8];  // one 64-coefficient int16 block per lane
     const JpegHuffFrame &F = P.frames[P.wg[2 * blockIdx.x]];
-    const int iv0 = P.wg[2 * blockIdx.x + 1], iv1 = min(iv0 + 64, F.n_iv);
-    const int a0 = F.iv_off[iv0] & ~15;
+    const int iv0 = P.wg[2 * blockIdx.x + 1], iv1 = min(iv0 + JH_LANES, F.n_iv);
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(F.tables);
         uint4 *dst = reinterpret_cast<uint4 *>(T);
         constexpr int n16 = (int)(8 * sizeof(JpegHuffTable) / 16);
-        for (int i = threadIdx.x; i < n16; i += 64) dst[i] = src[i];
-        zz[threadIdx.x] = kZigzag[threadIdx.x];
-        // the range + one look-ahead word (the device buffer has >= 32 B of slack past the end)
-        const int n16d = (F.iv_off[iv1] - a0 + 15) / 16 + 1;
-        const uint4 *d = reinterpret_cast<const uint4 *>(F.data + a0);
-        for (int i = threadIdx.x; i < n16d; i += 256) {
-            uint4 v[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-                if (i + 64 * u < n16d) v[u] = d[i + 64 * u];
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-                if (i + 64 * u < n16d)
-                    sdata[i + 64 * u] = make_uint4(bswap32(v[u].x), bswap32(v[u].y), bswap32(v[u].z), bswap32(v[u].w));
-        }
+        for (int i = threadIdx.x; i < n16; i += JH_LANES) dst[i] = src[i];
+        if (threadIdx.x < 64) zz[threadIdx.x] = kZigzag[threadIdx.x];
     }
     __syncthreads();
     const int iv = iv0 + threadIdx.x;
     if (iv >= iv1) return;
-    int bp = (F.iv_off[iv] - a0) * 8;
+    int bp = F.iv_off[iv] * 8;
     Window win;
-    win.init(reinterpret_cast<const uint32_t *>(sdata), ((F.iv_off[iv1] - a0 + 15) / 16 + 1) * 4 - 1, bp,
-             (F.iv_off[iv + 1] - a0) * 8);
+    win.init(F.words, F.nwords - 1, bp, F.iv_off[iv + 1] * 8);
     int4 *const mine = sblk[threadIdx.x];
     int16_t *const co = reinterpret_cast<int16_t *>(mine);
     int pred[3] = {0, 0, 0};
@@ -118,17 +105,23 @@ __global__ __launch_bounds__(64) void jpeg_huff_kernel(const JpegHuffParams P) {
     if (bad) P.error[P.wg[2 * blockIdx.x]] = 1;  // per frame of the call
 }
 
+// The call's interval bytes as big-endian dwords (what the bit window reads), per frame.
+__global__ __launch_bounds__(256) void jpeg_huff_bswap_kernel(const JpegHuffParams P) {
+    const JpegHuffFrame &F = P.frames[blockIdx.y];
+    if (F.nwords == 0) return;
+    const uint4 *src = reinterpret_cast<const uint4 *>(F.data);
+    uint4 *dst = reinterpret_cast<uint4 *>(F.words);
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < F.nwords / 4; i += gridDim.x * 256) {
+        const uint4 v = src[i];
+        dst[i] = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
+    }
+}
+
 }  // namespace
 
-int jpeg_huff_max_lds() { return 160 * 1024 - (int)(8 * sizeof(JpegHuffTable) + 64 + 64 * 128) - 1024; }
-
 const char *launch_jpeg_huff(const JpegHuffParams &p, hipStream_t s) {
-    static const bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void *>(jpeg_huff_kernel),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, jpeg_huff_max_lds()) == hipSuccess;
-    }();
-    (void)attr;
-    hipLaunchKernelGGL(jpeg_huff_kernel, dim3(p.n_wg), dim3(64), (size_t)p.lds_bytes, s, p);
+    hipLaunchKernelGGL(jpeg_huff_bswap_kernel, dim3(64, p.nframes), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(jpeg_huff_kernel, dim3(p.n_wg), dim3(JH_LANES), 0, s, p);
     return "jpeg_huff_kernel";
 }
 

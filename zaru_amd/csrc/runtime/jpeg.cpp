@@ -276,6 +276,8 @@ struct zr_jpeg_decoder {
     // self-synchronising device decoding (streams without restart intervals): per-segment states
     uint8_t *d_sync = nullptr;
     size_t sync_cap = 0;
+    uint8_t *d_hwords = nullptr;  // restart-interval frames' scans as big-endian dwords
+    size_t hwords_cap = 0;
     int *d_err = nullptr;         // [4096] per frame of the last call: set by jpeg_huff_kernel on a corrupt interval
     size_t n_last = 0;            // frames of the last call
     uint64_t n_gpu = 0, n_host = 0;
@@ -492,6 +494,7 @@ void zr_jpeg_decoder_destroy(zr_jpeg_decoder *d) {
     (void)hipHostFree(d->h_stage);
     (void)hipFree(d->d_stage);
     (void)hipFree(d->d_sync);
+    (void)hipFree(d->d_hwords);
     (void)hipFree(d->d_err);
     delete d;
 }
@@ -626,7 +629,7 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
             if (!gpu_entropy_enabled() || n_iv[f] < 8) n_iv[f] = 0;
             if (!n_iv[f]) continue;
             ob[f] = ((size_t)(n_iv[f] + 1) * 4 + 15) / 16 * 16;
-            groups += (size_t)(n_iv[f] + 63) / 64;
+            groups += (size_t)(n_iv[f] + zr::JH_LANES - 1) / zr::JH_LANES;
         }
         // streams without restart intervals: self-synchronising decoding (jpeg_sync.hip), its
         // staged scan padded to whole 64-segment workgroup ranges + the overrun margin
@@ -662,6 +665,10 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
                 stage += tb + spad[f];
             }
         // growing frees device buffers: the previous decode's kernels must be done with them
+        // the restart-interval frames' big-endian copies (bounded by their scans' sizes)
+        size_t hw_bytes = 0;
+        for (size_t f = 0; f < n; f++)
+            if (n_iv[f]) hw_bytes += ((lens[f] - hd[f].scan_begin) + 48 + 15) / 16 * 16;
         // per-segment device states of the sync frames (ck, exits x2, start, base, pred) + err_block
         size_t sync_bytes = 0;
         for (size_t f = 0; f < n; f++)
@@ -672,7 +679,8 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
             }
         if (sync_bytes) sync_bytes += 256;  // the per-pass change counters
         const bool grow = (size_t)blocks > dec->coef_cap || (size_t)pbytes > dec->planes_cap ||
-                          ((groups || nsync) && stage > dec->stage_cap) || sync_bytes > dec->sync_cap;
+                          ((groups || nsync) && stage > dec->stage_cap) || sync_bytes > dec->sync_cap ||
+                          hw_bytes > dec->hwords_cap;
         if (grow && hipEventSynchronize(dec->done) != hipSuccess) return err(ZR_ERR_DEVICE, "event sync failed");
         if ((size_t)blocks > dec->coef_cap) {
             (void)hipHostFree(dec->h_coef);
@@ -693,6 +701,14 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
             const size_t cap = (size_t)pbytes + (size_t)pbytes / 4;
             if (hipMalloc((void **)&dec->d_planes, cap) != hipSuccess) return err(ZR_ERR_DEVICE, "jpeg: out of memory");
             dec->planes_cap = cap;
+        }
+        if (hw_bytes > dec->hwords_cap) {
+            (void)hipFree(dec->d_hwords);
+            dec->d_hwords = nullptr;
+            dec->hwords_cap = 0;
+            const size_t cap = hw_bytes + hw_bytes / 4;
+            if (hipMalloc((void **)&dec->d_hwords, cap) != hipSuccess) return err(ZR_ERR_DEVICE, "jpeg: out of memory");
+            dec->hwords_cap = cap;
         }
         if (sync_bytes > dec->sync_cap) {
             (void)hipFree(dec->d_sync);
@@ -717,10 +733,11 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
         // unstuff the device frames' scans; a frame whose intervals do not match its DRI, or whose
         // 64-interval ranges exceed a workgroup's LDS, goes to the host path
         std::vector<int32_t> ivo;
-        int lds = 0;
         auto *fr = reinterpret_cast<zr::JpegHuffFrame *>(dec->h_stage);
         auto *wg = reinterpret_cast<int32_t *>(dec->h_stage + fb);
-        size_t n_wg = 0, used = fb + wb + sfb + swb;
+        size_t n_wg = 0, used = fb + wb + sfb + swb, hw = 0;
+        if (groups)
+            for (size_t f = 0; f < n; f++) fr[f] = zr::JpegHuffFrame{};  // (nwords = 0: not a device frame)
         for (size_t f = 0; f < n; f++) {
             if (!n_iv[f]) continue;
             uint8_t *const base = dec->h_stage + fofs[f];
@@ -728,16 +745,6 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
                 n_iv[f] = 0;
                 continue;
             }
-            int need = 0;
-            for (int g0 = 0; g0 < n_iv[f]; g0 += 64) {
-                const int r = ivo[std::min(g0 + 64, n_iv[f])] - (ivo[g0] & ~15);
-                need = std::max(need, ((r + 15) / 16 + 1) * 16);
-            }
-            if (need > zr::jpeg_huff_max_lds()) {
-                n_iv[f] = 0;
-                continue;
-            }
-            lds = std::max(lds, need);
             const size_t db = (size_t)ivo.back();
             auto *tabs = reinterpret_cast<zr::JpegHuffTable *>(base);
             for (int t = 0; t < 4; t++) {
@@ -752,6 +759,9 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
             F.tables = reinterpret_cast<const zr::JpegHuffTable *>(dbase);
             F.iv_off = reinterpret_cast<const int32_t *>(dbase + tb);
             F.data = dbase + tb + ob[f];
+            F.words = reinterpret_cast<uint32_t *>(dec->d_hwords + hw);
+            F.nwords = (int)((db + 48 + 15) / 16 * 4);
+            hw += (size_t)F.nwords * 4;
             F.coef = dec->d_coef + cofs[f] * 64;
             F.n_iv = n_iv[f];
             F.restart = hd[f].restart;
@@ -766,7 +776,7 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
                 F.coef_off[c] = P[f].coef_off[c];
                 F.bw[c] = P[f].bw[c];
             }
-            for (int g0 = 0; g0 < n_iv[f]; g0 += 64) {
+            for (int g0 = 0; g0 < n_iv[f]; g0 += zr::JH_LANES) {
                 wg[2 * n_wg] = (int32_t)f;
                 wg[2 * n_wg + 1] = g0;
                 n_wg++;
@@ -777,7 +787,6 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
         auto *sfr = reinterpret_cast<zr::JpegSyncFrame *>(dec->h_stage + fb + wb);
         auto *swg = reinterpret_cast<int32_t *>(dec->h_stage + fb + wb + sfb);
         size_t ns = 0, n_swg = 0, sy = 256;  // [0, 256): the change counters
-        int sync_lds = 0;
         for (size_t f = 0; f < n; f++) {
             if (!sync[f]) continue;
             uint8_t *const base = dec->h_stage + sofs[f];
@@ -831,7 +840,6 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
             }();
             F.warm = (int)std::min<int64_t>(zr::JS_WARM_MAX,
                                             std::max<int64_t>(zr::JS_WARM_MIN, (warm_blocks * bpb + 127) / 128 * 128));
-            sync_lds = std::max(sync_lds, F.warm / 8 + zr::JS_LANES * (zr::JS_SEG / 8) + zr::JS_MARGIN);
             F.coef = dec->d_coef + cofs[f] * 64;
             F.frame = (int)f;
             uint8_t *sp = dec->d_sync + sy;
@@ -889,7 +897,7 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
             hp.wg = reinterpret_cast<const int32_t *>(dec->d_stage + fb);
             hp.n_wg = (int)n_wg;
             hp.error = dec->d_err;
-            hp.lds_bytes = lds;
+            hp.nframes = (int)n;
             zr::launch_jpeg_huff(hp, st);
         }
         if (ns) {
@@ -899,7 +907,6 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
             sp.n_wg = (int)n_swg;
             sp.nframes = (int)ns;
             sp.error = dec->d_err;
-            sp.lds_bytes = sync_lds;
             sp.changed = reinterpret_cast<int *>(dec->d_sync);
             static_assert((zr::JS_PASSES + 1) * sizeof(int) <= 256, "change counters");
             if (hipMemsetAsync(dec->d_sync, 0, 256, st) != hipSuccess) return err(ZR_ERR_DEVICE, "jpeg: counter reset failed");

@@ -47,6 +47,8 @@ struct JpegHuffFrame {
     const JpegHuffTable *tables;  // [8]: DC 0..3, AC 0..3
     const int32_t *iv_off;        // [n_iv + 1] byte offsets of the intervals in `data` (+ end)
     const uint8_t *data;          // the intervals' unstuffed bytes, back to back (16-B aligned)
+    uint32_t *words;              // the same as big-endian dwords (jpeg_huff_bswap_kernel; 0: not a device frame)
+    int nwords;                   // a multiple of 4, with >= 32 B of zero slack past the data
     int16_t *coef;                // as JpegParams::coef
     int64_t coef_off[3];
     int n_iv, restart, nmcu, mcux, ncomp;
@@ -54,16 +56,16 @@ struct JpegHuffFrame {
     int bw[3];
 };
 
-// One launch decodes a batch of frames: workgroup w takes frame wg[2w]'s 64 intervals from
+// One launch decodes a batch of frames: workgroup w takes frame wg[2w]'s JH_LANES intervals from
 // wg[2w + 1] on.
+constexpr int JH_LANES = 256;
 struct JpegHuffParams {
     const JpegHuffFrame *frames;
     const int32_t *wg;            // [n_wg][2]
     int n_wg;
     int *error;                   // [frame of the call] set to 1 on a corrupt interval (bad code / AC index)
-    int lds_bytes;                // dynamic LDS: the largest 64-interval range, 16-B words + 1
+    int nframes;                  // frames[] entries (the call's frames; nwords = 0: not on this path)
 };
-int jpeg_huff_max_lds();          // the most dynamic LDS one workgroup may stage
 const char *launch_jpeg_huff(const JpegHuffParams &p, hipStream_t s);
 
 // Self-synchronising entropy decoding (jpeg_sync.hip) for streams without restart intervals:
@@ -112,7 +114,6 @@ struct JpegSyncParams {
     int n_wg, nframes;
     int *error;                   // [frame of the call]
     int *changed;                 // [JS_PASSES + 1] exits changed per pass (zeroed per call)
-    int lds_bytes;                // dynamic LDS: the largest warm-up + 64 segments + margin of the call
 };
 constexpr int JS_PASSES = 32;     // sync passes launched per call at most (each returns at once
                                   // once a pass changed nothing)
