@@ -13,7 +13,7 @@ from zaru_amd.nn import model_bytes  # noqa: E402
 model, trace = sys.argv[1], sys.argv[2]
 batch = int(sys.argv[3]) if len(sys.argv) > 3 else 341
 plan = [l for l in plan_describe(model_bytes(model)).splitlines()
-        if l.split(" ", 1)[0] not in ("input", "output")]
+        if l.split(" ", 1)[0] not in ("input", "output") and not l.endswith(" grp=0")]  # grouped into the previous launch
 rows = [r for r in csv.DictReader(open(trace)) if "zr::" in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 rows = rows[-len(plan):]
