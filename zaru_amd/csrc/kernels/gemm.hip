@@ -157,8 +157,7 @@ __global__ __launch_bounds__(256) void gemm_smallk_group_kernel(const LaunchGrou
 // 16-byte loads (one wave instruction moves a whole 1 KiB row segment), double-buffered with
 // the next K-chunk's loads in flight during the current chunk's MFMAs.  Each wave owns NT
 // 32-column tiles x MT 32-row tiles, so every A fragment feeds NT MFMAs and every B fragment MT.
-// Block -> tile mapping is XCD-aware: the M-blocks of one column tile are 8 launch slots apart,
-// i.e. on the same XCD under round-robin dispatch, so their shared X tile is an L2 hit.
+// Block -> tile mapping is XCD-aware (see gemm_tiled_body).
 constexpr int TKC = 16;  // K rows per stage
 
 // vec: the output tile leaves through LDS as 16-byte row segments (a wave's 32x32 tile in 4
@@ -167,22 +166,19 @@ constexpr int TKC = 16;  // K rows per stage
 // (<1,1>: the skinny store-bound expand convs -- 4 waves per SIMD fit without spills and hide
 // more of the store latency than 3)
 template <int MT, int NT, bool RES>
-__device__ __forceinline__ void gemm_tiled_body(const GemmParams &P, int mblocks, int nct, int vec, int bx) {
+__device__ __forceinline__ void gemm_tiled_body(const GemmParams &P, int mblocks, int nct, int vec, int bx, int gx) {
     constexpr int BN = 4 * NT * 32, MR = MT * 32;
     constexpr int XV = TKC * BN / 4 / 256;  // float4 of X staged per thread per chunk
     constexpr int WV = (TKC * MR / 4 + 255) / 256;
     __shared__ __attribute__((aligned(16))) float sX[2][TKC][BN];
     __shared__ __attribute__((aligned(16))) float sW[2][TKC][MR];
 
-    int ct, mb;
-    if (mblocks == 1) {
-        ct = bx;
-        mb = 0;
-    } else {
-        const int g = bx / (8 * mblocks), r = bx - g * 8 * mblocks;
-        mb = r >> 3;
-        ct = g * 8 + (r & 7);
-    }
+    // XCD-contiguous: launch slot bx runs on XCD bx % 8 (round-robin dispatch), and each XCD
+    // takes one contiguous eighth of the (column tile, M block) pairs, M blocks innermost -- the
+    // M blocks of a column tile share its X tile in that XCD's L2, and the XCD's output rows
+    // leave as long runs of adjacent segments.
+    const int idx = (bx & 7) * (gx >> 3) + (bx >> 3);
+    const int ct = idx / mblocks, mb = idx - ct * mblocks;
     if (ct >= nct) return;  // whole workgroup, before any barrier
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int kh = lane >> 5, col = lane & 31;
@@ -295,14 +291,14 @@ __device__ __forceinline__ void gemm_tiled_body(const GemmParams &P, int mblocks
 template <int MT, int NT, bool RES>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MT * NT == 1 ? 4 : 1)))
 void gemm_tiled_kernel(const GemmParams P, int mblocks, int nct, int vec) {
-    gemm_tiled_body<MT, NT, RES>(P, mblocks, nct, vec, blockIdx.x);
+    gemm_tiled_body<MT, NT, RES>(P, mblocks, nct, vec, blockIdx.x, gridDim.x);
 }
 
 template <int MT, int NT, bool RES>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MT * NT == 1 ? 4 : 1)))
 void gemm_tiled_group_kernel(const LaunchGroup<GemmParams> G) {
     const GroupSlot t = group_slot(G);
-    gemm_tiled_body<MT, NT, RES>(G.p[t.g], G.a0[t.g], G.a1[t.g], G.a2[t.g], t.bx);
+    gemm_tiled_body<MT, NT, RES>(G.p[t.g], G.a0[t.g], G.a1[t.g], G.a2[t.g], t.bx, G.gx[t.g]);
 }
 
 // ---------------------------------------------------------------- image-row variant
@@ -448,7 +444,7 @@ static GemmChoice choose_gemm(const GemmParams &p) {
                         p.o_sC % 4 == 0 && ((uintptr_t)p.out % 16) == 0;
         c.form = GF_TILED;
         c.v0 = mt, c.v1 = nt, c.v2 = p.res_mode != 0;
-        c.gx = mblocks == 1 ? nct : ((nct + 7) / 8) * 8 * mblocks;
+        c.gx = (nct * mblocks + 7) / 8 * 8;
         c.a0 = mblocks, c.a1 = nct, c.a2 = vec;
         return c;
     }
