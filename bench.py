@@ -474,7 +474,7 @@ def main():
                 dist.broadcast(uid, 0)
                 comms.append(Comm(bytes(uid.numpy().tobytes()), world, rank, device))
         else:
-            gather = shard.RecordGather(args.batch * len(wls), shard.record_width(), "cpu")
+            gather = shard.RecordGather(args.batch * len(wls), shard.record_width())
     if world == 1 and args.self_gather:  # the N > 1 data path on one GPU: a one-rank communicator
         comms = [Comm(Comm.unique_id(), 1, 0, device) for _ in wls]
     if world > 1 or comms:

@@ -112,7 +112,11 @@ int zr_detection_candidates_async(const float *d_logits, const float *d_boxes, u
  * first dcap of them in d_dets [n][dcap][20] = {conf, angle, cx, cy, w, h, 7 x (kx, ky)} (frame
  * px, keypoints past the network's zero; dcap = anchors keeps every detection), and when d_records
  * is not NULL the all-gather record [n][2 + 20 rmax] = {frame id first_id + f * id_stride (u32
- * bits), count (u32 bits), the first rmax detections, zeros}. */
+ * bits), count (u32 bits), the first rmax detections, zeros}.  d_ties (may be NULL):
+ * [n][2] = {candidates (conf >= thresh), candidates whose confidence another candidate shares};
+ * ties are ordered by anchor index, which is Rust's sort_unstable order only up to 20
+ * candidates (nms.rs:66), so a frame with more than 20 candidates and a tie is not pinned by the
+ * reference. */
 typedef struct {
     int face;               /* 1 BlazeFace (angle: eye line vs +X), 0 BlazePalm (wrist -> MCP vs +Y) */
     int anchors, params, keypoints;  /* A, values per anchor (16 / 18), keypoints (6 / 7) */
@@ -123,7 +127,16 @@ typedef struct {
 int zr_detect_post_async(const float *d_logits, const float *d_boxes, const float *d_anchors,
                          const float *d_letterbox, size_t n, const zr_detpost_cfg *cfg,
                          int32_t *d_count, float *d_dets, size_t dcap, float *d_records, size_t rmax,
-                         uint32_t first_id, uint32_t id_stride, void *hip_stream);
+                         uint32_t first_id, uint32_t id_stride, int32_t *d_ties, void *hip_stream);
+
+/* The same over a device-resident frame subset: frame f < *d_nframes (f < n) is the logits /
+ * boxes row f, and its count / detections / tie counts / letterbox go to slot d_map[f]; slots of
+ * other frames are left as they are (the device HandTracker's palm detection over the streams
+ * due for it, hand/tracking.rs:210-218). */
+int zr_detect_post_mapped_async(const float *d_logits, const float *d_boxes, const float *d_anchors,
+                                const float *d_letterbox, size_t n, const int32_t *d_map, const int32_t *d_nframes,
+                                const zr_detpost_cfg *cfg, int32_t *d_count, float *d_dets, size_t dcap,
+                                int32_t *d_ties, void *hip_stream);
 
 /* ---- the one collective of the multi-GPU path ------------------------------
  * A communicator over the node's ranks (one process per GPU) for the all-gather of the detection
@@ -135,7 +148,12 @@ typedef struct zr_comm zr_comm;
 int zr_comm_unique_id(uint8_t id[128]);
 int zr_comm_create(const uint8_t id[128], int nranks, int rank, int device, zr_comm **out);
 void zr_comm_destroy(zr_comm *c);
-/* recv (nranks * bytes, rank-major) <- every rank's send (bytes), enqueued on hip_stream */
+/* the communicator's rank count (what an all-gather writes nranks * bytes for) */
+int zr_comm_size(const zr_comm *c, int *nranks);
+/* recv (nranks * bytes, rank-major) <- every rank's send (bytes), enqueued on hip_stream.
+ * Every zr_comm_* call first takes the thread's pending HIP error (hipGetLastError) and, if one
+ * is set, returns ZR_ERR_DEVICE naming it without calling RCCL; after an RCCL call it clears
+ * only the status RCCL itself left. */
 int zr_comm_all_gather_async(zr_comm *c, const void *d_send, void *d_recv, size_t bytes, void *hip_stream);
 
 /* ---- LandmarkTracker state on the device ------------------------------
@@ -235,6 +253,18 @@ int zr_hand_manage_async(zr_track_state *d_state, uint64_t *d_ids, float *d_hroi
 int zr_cnn_estimate_device_views_async(zr_session *s, const zr_frame *frames, size_t n_frames,
                                        const zr_view_desc *d_views, size_t n_views, float lo,
                                        float hi, float *const *d_outputs, void *hip_stream);
+/* The same when only the first *d_count (device int, <= n_views) views are needed: the launches
+ * skip the work of images at and past it, whose outputs are then undefined.  The count is read
+ * by the kernels, so no host decision sits between the step that writes it and this one. */
+int zr_cnn_estimate_device_views_count_async(zr_session *s, const zr_frame *frames, size_t n_frames,
+                                             const zr_view_desc *d_views, size_t n_views, const int32_t *d_count,
+                                             float lo, float hi, float *const *d_outputs, void *hip_stream);
+/* The streams zr_hand_manage_async asked to detect on (d_det_pending[s] != 0) compacted in stream
+ * order: d_due[k] = s and d_due_views[k] = *view_template with its frame index set to s, for
+ * k < *d_ndue (one workgroup, on the stream; hand/tracking.rs:210-218's schedule on the device).
+ * d_total (may be NULL): *d_total += *d_ndue, a running count of the detections run. */
+int zr_due_compact_async(const int32_t *d_det_pending, size_t n, const zr_view_desc *view_template, int32_t *d_due,
+                         int32_t *d_ndue, zr_view_desc *d_due_views, uint64_t *d_total, void *hip_stream);
 
 /* ---- JPEG frame source --------------------------------------------------
  * Replaces decode_jpeg (crates/zaru-image/src/jpeg.rs:107-182) for its libjpeg-turbo backend
@@ -273,9 +303,11 @@ typedef struct {
  * NULL; waits for the last call) is 1 when a frame of the LAST call held an invalid Huffman code or
  * AC index.  Error contract: a frame decoded on the host with corrupt data fails the call
  * (ZR_ERR_INVALID_ARGUMENT, frame named); on the device it cannot fail the already-returned call,
- * so the rest of the corrupt interval (a stream without restart intervals: every block from the
- * bad one to the end of the frame) decodes as all-zero blocks (libjpeg-turbo's insufficient-data
- * behaviour) and the frame's flag is set -- zr_jpeg_frame_errors names the frames. */
+ * so the block holding the bad code and the rest of its interval (a stream without restart
+ * intervals: every block from the bad one to the end of the frame) decode as all-zero blocks
+ * (libjpeg-turbo's insufficient-data behaviour) and the frame's flag is set --
+ * zr_jpeg_frame_errors names the frames.  A valid stream without restart intervals whose device
+ * sync passes do not converge is finished by a serial decode on the device: never flagged. */
 int zr_jpeg_decoder_status(zr_jpeg_decoder *d, uint64_t *gpu_entropy, uint64_t *host_entropy, int *corrupt);
 /* per frame of the last call: 1 = corrupt entropy data (waits for that call); *n = its frame count */
 int zr_jpeg_frame_errors(zr_jpeg_decoder *d, int32_t *flags, size_t cap, size_t *n);

@@ -121,6 +121,8 @@ def _lib():
     L.zo_detector_map.argtypes = [P, sz, C.POINTER(Rect), u32]
     L.zo_detect_post.restype = sz
     L.zo_detect_post.argtypes = [C.c_int, P, P, sz, u32, u32, u32, u32, f, f, P, sz]
+    L.zo_detect_post_mode.restype = sz
+    L.zo_detect_post_mode.argtypes = [C.c_int, P, P, sz, u32, u32, u32, u32, f, f, C.c_int, P, sz]
     L.zo_estimator_map.argtypes = [P, sz, C.POINTER(Rect), u32]
     L.zo_tracker_update.restype = C.c_int
     L.zo_tracker_update.argtypes = [P, sz, C.POINTER(RRect), f, f, f, C.POINTER(RRect),
@@ -258,13 +260,14 @@ def nms(dets, iou_thresh=0.3, mode=1):
     return [out[i] for i in range(n)]
 
 
-def detect_post(kind, boxes, confs, img_w, img_h, in_w, in_h, thresh=0.5, iou_thresh=0.3):
+def detect_post(kind, boxes, confs, img_w, img_h, in_w, in_h, thresh=0.5, iou_thresh=0.3, remove=False):
+    """remove: SuppressionMode::Remove (nms.rs:70-76) instead of the default Average."""
     boxes = np.ascontiguousarray(boxes, np.float32)
     confs = np.ascontiguousarray(confs, np.float32).reshape(-1)
     na = confs.shape[0]
     out = (Det * na)()
-    n = _lib().zo_detect_post(kind, _ptr(boxes), _ptr(confs), na, img_w, img_h, in_w, in_h,
-                              thresh, iou_thresh, out, na)
+    n = _lib().zo_detect_post_mode(kind, _ptr(boxes), _ptr(confs), na, img_w, img_h, in_w, in_h,
+                                   thresh, iou_thresh, 0 if remove else 1, out, na)
     return [out[i] for i in range(n)]
 
 

@@ -392,6 +392,13 @@ void zo_detector_map(zo_det *dets, size_t n, const zo_rect *rect, uint32_t in_w)
 size_t zo_detect_post(int kind, const float *boxes, const float *confs, size_t nanchors,
                       uint32_t img_w, uint32_t img_h, uint32_t in_w, uint32_t in_h,
                       float thresh, float iou, zo_det *out, size_t cap) {
+    return zo_detect_post_mode(kind, boxes, confs, nanchors, img_w, img_h, in_w, in_h, thresh, iou, 1, out, cap);
+}
+
+/* the same with SuppressionMode (nms.rs:154-163: 0 Remove, 1 Average) */
+size_t zo_detect_post_mode(int kind, const float *boxes, const float *confs, size_t nanchors,
+                           uint32_t img_w, uint32_t img_h, uint32_t in_w, uint32_t in_h,
+                           float thresh, float iou, int mode, zo_det *out, size_t cap) {
     uint32_t face_layers[] = {2, 16, 16, 6, 8, 8};   /* face/detection.rs:53 */
     uint32_t palm_layers[] = {2, 24, 24, 6, 12, 12}; /* hand/detection.rs:117 */
     uint32_t full_layers[] = {1, 48, 48};            /* face/detection.rs:86-88 */
@@ -404,7 +411,7 @@ size_t zo_detect_post(int kind, const float *boxes, const float *confs, size_t n
     zo_det *tmp = (zo_det *)malloc(sizeof(zo_det) * na);
     size_t n = zo_extract(kind, boxes, confs, na, anchors, in_w, in_h, thresh, tmp, na);
     zo_det *nms = (zo_det *)malloc(sizeof(zo_det) * (n ? n : 1));
-    size_t m = zo_nms(tmp, n, iou, 1, nms);
+    size_t m = zo_nms(tmp, n, iou, mode, nms);
     zo_rect full = zo_rect_from_top_left(0.0f, 0.0f, (float)img_w, (float)img_h);
     zo_rect rect = zo_rect_grow_to_fit_aspect(full, in_w, in_h);
     zo_detector_map(nms, m, &rect, in_w);

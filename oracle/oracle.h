@@ -77,6 +77,9 @@ void zo_detector_map(zo_det *dets, size_t n, const zo_rect *rect, uint32_t in_w)
 size_t zo_detect_post(int kind, const float *boxes, const float *confs, size_t nanchors,
                       uint32_t img_w, uint32_t img_h, uint32_t in_w, uint32_t in_h,
                       float thresh, float iou, zo_det *out, size_t cap);
+size_t zo_detect_post_mode(int kind, const float *boxes, const float *confs, size_t nanchors,
+                           uint32_t img_w, uint32_t img_h, uint32_t in_w, uint32_t in_h,
+                           float thresh, float iou, int mode, zo_det *out, size_t cap);
 
 /* Estimator::estimate_impl map-out (landmark.rs:314-348): positions in place, n x 3 */
 void zo_estimator_map(float *pos, size_t n, const zo_rect *view_local_rect, uint32_t in_w);

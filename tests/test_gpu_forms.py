@@ -44,7 +44,8 @@ SWITCHES = {
     "no_ws": "-ws",
     "no_groups": "-groups",
     "no_dwgap": "-dwgap",
-    "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws,-groups,-dwgap",
+    "no_rt": "-rt",
+    "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws,-groups,-dwgap,-rt",
 }
 
 
@@ -135,3 +136,44 @@ def test_ws_form_is_bitwise_neutral(tmp_path):
     for k in res["default"]:
         if k != "kernels":
             assert np.array_equal(res["default"][k], res["no_ws"][k]), (k, float(np.abs(res["default"][k] - res["no_ws"][k]).max()))
+
+
+# The row-task depthwise (form "rt", dwpw_dma_body RT > 0) picks its task width from the layer's
+# column tile, which depends on the batch: the bench's batches (palm 256 / 85 frames, hand 341
+# ROIs, FaceMesh and BlazeFace 341 images) exercise the 2-, 4- and 8-wide tasks.
+RT_CHILD = r"""
+import sys, ctypes as C, numpy as np
+sys.path.insert(0, sys.argv[1])
+from zaru_amd.nn import NeuralNetwork, model_bytes
+from zaru_amd._lib import lib, check
+out, kernels = {}, []
+for model, s, b in (("palm_detection_lite", 192, 256), ("palm_detection_lite", 192, 85),
+                    ("hand_landmark_lite", 224, 341), ("face_landmark", 192, 341),
+                    ("face_detection_short_range", 128, 341)):
+    net = NeuralNetwork.from_onnx(model_bytes(model)).load()
+    check(lib().zr_profile_enable(net._h, 1))
+    x = np.random.default_rng(b).uniform(-1.0, 1.0, size=(b, 3, s, s)).astype(np.float32)
+    for i, o in enumerate(net.estimate(x)):
+        out[f"{model}/{b}/{i}"] = o
+    need = C.c_size_t()
+    buf = C.create_string_buffer(1 << 20)
+    check(lib().zr_profile_read(net._h, buf, len(buf), C.byref(need)))
+    kernels += [l.split()[0] for l in buf.value.decode().splitlines() if l.strip()]
+np.savez(sys.argv[2], kernels=np.array(kernels), **out)
+"""
+
+
+def test_rt_form_is_bitwise_neutral_at_bench_batches(tmp_path):
+    res = {}
+    for name, env in (("default", ""), ("no_rt", "-rt")):
+        path = str(tmp_path / f"{name}.npz")
+        subprocess.run([sys.executable, "-c", RT_CHILD, REPO, path], env=dict(os.environ, ZARU_HIP_FORMS=env),
+                       check=True, timeout=110)
+        with np.load(path) as z:
+            res[name] = {k: z[k] for k in z.files}
+    widths = {k.rsplit(",", 1)[-1].rstrip(">") for k in res["default"]["kernels"] if k.startswith("dwpw_dma")}
+    assert {"2", "8"} <= widths, widths  # row tasks of 2 (12^2 / 6^2 / 14^2) and 8 (palm 48^2 / 24^2)
+    assert {k.rsplit(",", 1)[-1].rstrip(">") for k in res["no_rt"]["kernels"] if k.startswith("dwpw_dma")} == {"0"}
+    for k in res["default"]:
+        if k != "kernels":
+            assert np.array_equal(res["default"][k], res["no_rt"][k]), (k, float(np.abs(res["default"][k] - res["no_rt"][k]).max()))

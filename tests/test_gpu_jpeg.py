@@ -281,6 +281,17 @@ def test_corrupt_interval_leaves_no_stale_coefficients(dec):
         used.close()
 
 
+def test_corrupt_interval_zeroes_the_bad_block(dec):
+    """the restart-interval decoder applies the sync decoder's rule -- the block holding
+    the bad code is zero too, not a partial decode (grayscale noise, 2-block intervals)."""
+    from test_gpu_jpeg_sync import check_bad_block_rule, noise
+    data = encode(noise(240, 320, 24, gray=True), quality=90, restart_marker_blocks=8)
+    bad = _corrupt_third_interval(data)
+    got = dec.decode(bad)
+    assert list(dec.frame_errors()) == [True]
+    check_bad_block_rule(libjpeg_turbo_rgba(data), got)
+
+
 def test_restart_stream_cut_mid_scan(dec):
     """A restart-interval stream cut inside the scan no longer has one RSTn per interval: it
     takes the host path, which pads with zero bits or rejects it, and never reads past the

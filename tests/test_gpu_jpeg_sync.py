@@ -32,7 +32,15 @@ CASES = [
     (lambda: synthetic(500, 700, 20)[..., 1], {"quality": 85}, True),
     # ~700 bits per block (q100 noise): over JS_MAX_BITS_PER_BLOCK, the host decodes it
     (lambda: noise(600, 800, 14), {"quality": 100, "subsampling": 0}, False),
+    # ~591 bits per block (q99, 80 % noise): just under the gate, the densest scan the device takes
+    (lambda: dense(600, 800, 14), {"quality": 99, "subsampling": 0}, True),
 ]
+
+
+def dense(h, w, seed):
+    yy, xx = np.mgrid[0:h, 0:w]
+    sm = np.stack([128 + 100 * np.sin(xx / 37.0), 128 + 100 * np.cos(yy / 23.0), 128 + 80 * np.sin((xx + yy) / 51.0)], -1)
+    return np.clip(0.8 * noise(h, w, seed).astype(float) + 0.2 * sm, 0, 255).astype(np.uint8)
 
 
 @pytest.mark.parametrize("case", range(len(CASES)))
@@ -93,6 +101,76 @@ def test_sync_corrupt_scan_is_flagged_and_zero_filled():
         assert d.status()[2] == 1
         assert list(d.frame_errors()) == [True]
         assert (got[-16:, :, :3] == 128).all()
+    finally:
+        d.close()
+
+
+def _run_with_env(code, env):
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code, repo], env=dict(os.environ, **env),
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return r.stdout
+
+
+@pytest.mark.parametrize("passes", [0, 1])
+def test_sync_passes_that_run_out_finish_serially(passes):
+    """a valid scan whose sync passes end with lanes still out of step is finished by
+    the serial kernel from the last in-step lane's exit -- byte-equal, not flagged, no zero fill.
+    ZARU_JPEG_SYNC_PASSES caps the passes so that these frames (and the dense one just under the
+    600 bits/block gate, where out-of-step chains are longest) really take that path."""
+    code = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + "/tests")
+from test_gpu_jpeg import encode, synthetic, libjpeg_turbo_rgba
+from test_gpu_jpeg_sync import dense
+from zaru_amd.jpeg import JpegDecoder
+d = JpegDecoder(0)
+for data in (encode(synthetic(360, 480, 5), quality=90), encode(dense(240, 320, 3), quality=99, subsampling=0)):
+    got = d.decode(data)
+    assert np.array_equal(got, libjpeg_turbo_rgba(data))
+    assert not any(d.frame_errors()), list(d.frame_errors())
+print("ok", d.status())
+"""
+    out = _run_with_env(code, {"ZARU_JPEG_SYNC_PASSES": str(passes)})
+    assert out.startswith("ok (2, 0, 0)"), out
+
+
+def _blocks(img):
+    h, w = img.shape[0] // 8 * 8, img.shape[1] // 8 * 8
+    return img[:h, :w, 0].reshape(h // 8, 8, w // 8, 8).transpose(0, 2, 1, 3).reshape(-1, 64)
+
+
+def check_bad_block_rule(clean, bad):
+    """Grayscale frames: every 8x8 block of the corrupt decode equals the clean decode or is flat
+    mid-grey (an all-zero coefficient block), the changed blocks are all flat -- the block holding
+    the bad code included, with no partial decode kept -- and some block changed."""
+    c, b = _blocks(clean), _blocks(bad)
+    same = (c == b).all(1)
+    flat = (b == 128).all(1)
+    assert (~same).any()
+    assert (same | flat).all(), np.flatnonzero(~(same | flat))[:8]
+    assert not (flat & (c == 128).all(1)).any()  # noise: no clean block is flat by chance
+
+
+def test_sync_corrupt_gray_zeroes_the_bad_block():
+    from zaru_amd.jpeg import JpegDecoder
+    data = encode(noise(240, 320, 23, gray=True), quality=90)
+    bad = bytearray(data)
+    k = _scan_start(data)
+    mid = k + (len(data) - k) // 2
+    while data[mid - 1] == 0xFF:
+        mid += 1
+    bad[mid:mid + 16] = b"\xff\x00" * 8
+    d = JpegDecoder(0)
+    try:
+        got = d.decode(bytes(bad))
+        assert list(d.frame_errors()) == [True]
+        check_bad_block_rule(libjpeg_turbo_rgba(data), got)
+        assert (_blocks(got)[-1] == 128).all()  # zero to the end of the frame
     finally:
         d.close()
 

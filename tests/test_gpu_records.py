@@ -5,6 +5,9 @@ post-processing options of Detector (crates/zaru/src/detection.rs:44-111,186-202
   records the host packs from the pipeline's detections (`pack_detection_records`, the record
   layout of zaru_amd/shard.py), for face and palm frames;
 * a one-rank communicator (zr_comm_*, RCCL) gathers exactly this rank's records, step after step;
+  a world that is not the communicator's rank count is refused (the gather would write past the
+  receive block), and a HIP error pending from earlier work is reported by the next zr_comm_*
+  call instead of being cleared with RCCL's own stale status;
 * SuppressionMode::Remove (nms.rs:70-76) on the device equals the host restatement;
 * the default detection capacity keeps every NMS output (the reference's Detections is a Vec),
   and a smaller cap reports what it drops.
@@ -80,6 +83,36 @@ def test_one_rank_communicator_gathers_the_records(frames):
         p.step(k + 1 < 4)
         assert np.array_equal(p.gathered().view(np.uint32), p.records().view(np.uint32)), k
     del p
+    comm.close()
+
+
+def test_records_world_must_match_the_communicator(frames):
+    import zaru_amd.host as H_
+    from zaru_amd._lib import Comm
+    _, flist, forced = frames
+    comm = Comm(Comm.unique_id(), 1, 0, 0)
+    assert comm.size() == 1
+    p = _pipe(H_, "face")
+    p.set_frames(flist, forced)
+    with pytest.raises(Exception, match="rank count"):
+        p.enable_records(8, 0, 1, comm.ptr, 2)
+    del p
+    comm.close()
+
+
+def test_comm_reports_a_pending_hip_error():
+    import ctypes
+    from zaru_amd._lib import Comm, DeviceBuffer, ZaruError
+    comm = Comm(Comm.unique_id(), 1, 0, 0)
+    src, dst = DeviceBuffer(256), DeviceBuffer(256)
+    hip = ctypes.CDLL("libamdhip64.so")
+    assert hip.hipSetDevice(ctypes.c_int(4096)) != 0  # a failed HIP call: its error is now pending
+    with pytest.raises(ZaruError, match="pending HIP error") as e:
+        comm.all_gather_async(src.ptr, dst.ptr, 256)
+    assert e.value.code == -3
+    comm.all_gather_async(src.ptr, dst.ptr, 256)  # taken once: the next call runs
+    from zaru_amd._lib import synchronize
+    synchronize()
     comm.close()
 
 

@@ -100,7 +100,7 @@ def _gather_worker(rank, world, port, steps, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         B = 6
-        g = shard.RecordGather(B, shard.record_width(), "cpu")
+        g = shard.RecordGather(B, shard.record_width())
         got = []
         t0 = time.perf_counter()
         for k in range(steps):
@@ -159,7 +159,7 @@ def _combined_worker(rank, world, port, steps, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         B = 5
-        g = shard.RecordGather(2 * B, shard.record_width(), "cpu")
+        g = shard.RecordGather(2 * B, shard.record_width())
         got = []
         for k in range(steps):
             face_ids = [rank + world * i for i in range(B)]

@@ -10,7 +10,7 @@ i=0
 for F in "$@"; do
   for MB in $MODELS; do
     M=${MB%%:*}; B=${MB##*:}
-    O=gpurun_out/$TAG/$i/$M; mkdir -p $O
+    O=gpurun_out/$TAG/$i/${M}_$B; mkdir -p $O
     ( [ -n "$F" ] && export $F; timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O -o trace -- \
       python3 tools/kernel_probe.py $M $B 5 > /dev/null 2> $O/err.txt ) || { echo "probe $M failed ($F)"; exit 1; }
   done

@@ -16,6 +16,9 @@ the GPU box never runs this).  Everything it writes is data:
                           the f64-oracle outputs (SURVEY.md §8c fixture F2).
 * decode_cases.npz     -- raw detector outputs (real + crafted overlapping candidates) with the
                           oracle's decoded, NMS'd, image-mapped detections (fixture F3).
+* nms_ties.npz         -- > 20 saturated (1.0f) tied candidates per frame, Average and Remove
+                          mode outputs of the oracle (anchor-order ties; unpinned by Rust above
+                          20 candidates).  `python tools/make_golden.py ties` remakes only this.
 
 JPEG decoding here uses PIL/libjpeg; the reference uses zune-jpeg, so pixels may differ by
 +-1.  That is why fixtures store decoded colour codes, never the JPEG.
@@ -283,6 +286,51 @@ def decode_cases():
     np.savez_compressed(os.path.join(GOLD, "decode_cases.npz"), **cases)
 
 
+def nms_ties():
+    """Fixture nms_ties.npz: frames with more than 20 candidates of exactly equal,
+    saturated confidence (logit 40 -> sigmoid 1.0f), in overlapping clusters whose members differ
+    in box and keypoints, so the order inside a group changes the weighted sums' bits.  Expected
+    outputs are the oracle's, i.e. ties in anchor order (a stable sort).  Rust's sort_unstable is
+    stable only up to 20 elements (nms.rs:66); above that its order for these ties is NOT pinned
+    by the reference: the fixture pins this build's documented rule, not the reference's."""
+    cases = {}
+    rng = np.random.default_rng(0x71E5)
+    for kind, name, na, npar, side in ((O.FACE, "face", 896, 16, 128), (O.PALM, "palm", 2016, 18, 192)):
+        for case in range(2):
+            boxes = rng.normal(0, 3, size=(na, npar)).astype(np.float32)
+            logits = np.full(na, -20.0, np.float32)
+            for c in range(4 + case):  # clusters of 7-9 saturated candidates
+                a = int(rng.integers(20, na - 20))
+                members = sorted(set(rng.integers(a - 15, a + 15, size=9).tolist()))
+                size = float(rng.uniform(10, 40))
+                for j in members:
+                    logits[j] = np.float32(40.0)
+                    boxes[j, 0:2] = rng.normal(0, 1.0, 2)
+                    boxes[j, 2:4] = size * rng.uniform(0.9, 1.1, 2)
+            for j in rng.integers(0, na, size=3):  # a few unsaturated ones
+                logits[j] = np.float32(rng.uniform(0.5, 3.0))
+            img = np.array([int(rng.integers(200, 2000)), int(rng.integers(200, 2000))])
+            key = f"{name}_{case}"
+            cases[f"{key}/boxes"], cases[f"{key}/logits"], cases[f"{key}/img"] = boxes, logits, img
+            conf = np.array([O.sigmoid(float(v)) for v in logits], np.float32)
+            cand = conf[conf >= 0.5]
+            _, inv, cnt = np.unique(cand.view(np.uint32), return_inverse=True, return_counts=True)
+            cases[f"{key}/ties"] = np.array([len(cand), int((cnt[inv] > 1).sum())], np.int32)
+            for mode in ("average", "remove"):
+                dets = O.detect_post(kind, boxes, logits, int(img[0]), int(img[1]), side, side,
+                                     remove=mode == "remove")
+                rec = np.zeros((len(dets), 6 + 2 * 7), np.float32)
+                for i, d in enumerate(dets):
+                    rec[i, 0], rec[i, 1] = d.conf, d.angle
+                    rec[i, 2:6] = d.rect.tuple()
+                    for k in range(d.nkp):
+                        rec[i, 6 + 2 * k], rec[i, 7 + 2 * k] = d.kp[k][0], d.kp[k][1]
+                cases[f"{key}/want_{mode}"] = rec
+            print("ties case", key, cases[f"{key}/ties"], len(cases[f"{key}/want_average"]),
+                  len(cases[f"{key}/want_remove"]))
+    np.savez_compressed(os.path.join(GOLD, "nms_ties.npz"), **cases)
+
+
 # ------------------------------------------------------------------ SURVEY 8(f)-1 networks
 NEXT_SPECS = {  # BlazeFace full range (face/detection.rs:61-94), FaceMesh V2 (mediapipe.rs:81-116)
     "face_detection_full_range": ("face_detection_full_range.onnx", 192, -1.0, 1.0),
@@ -361,6 +409,9 @@ def main():
     if sys.argv[1:] == ["next"]:
         next_models()
         return
+    if sys.argv[1:] == ["ties"]:
+        nms_ties()
+        return
     os.makedirs(GOLD, exist_ok=True)
     with open(os.path.join(GOLD, "reference_kat.json"), "w") as f:
         json.dump(reference_kat(), f, indent=1)
@@ -369,6 +420,7 @@ def main():
     sad_linus_mesh()
     models_f64()
     decode_cases()
+    nms_ties()
     next_models()
 
 

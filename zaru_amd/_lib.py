@@ -53,13 +53,17 @@ SIGNATURES = [
     ("zr_track_seed_async", _I, [_P, _SZ, _P, _P, _P]),
     ("zr_track_update_async", _I, [_P, _SZ, _P, _P, _SZ, _P, _SZ, _P, _P, _P]),
     ("zr_view_describe", _I, [_P, _SZ, _U32, _P]),
-    ("zr_detect_post_async", _I, [_P, _P, _P, _P, _SZ, _P, _P, _P, _SZ, _P, _SZ, _U32, _U32, _P]),
+    ("zr_detect_post_async", _I, [_P, _P, _P, _P, _SZ, _P, _P, _P, _SZ, _P, _SZ, _U32, _U32, _P, _P]),
+    ("zr_detect_post_mapped_async", _I, [_P, _P, _P, _P, _SZ, _P, _P, _P, _P, _P, _SZ, _P, _P]),
+    ("zr_due_compact_async", _I, [_P, _SZ, _P, _P, _P, _P, _P, _P]),
+    ("zr_cnn_estimate_device_views_count_async", _I, [_P, _P, _SZ, _P, _SZ, _P, _F, _F, _P, _P]),
     ("zr_track_seed_detections_async", _I, [_P, _P, _SZ, _P, _P, _P, _SZ, _P, _F, _I, _P, _P, _P, _P]),
     ("zr_hand_manage_async", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P, _SZ, _P, C.c_double, _I,
                                   _P, _P, _P]),
     ("zr_comm_unique_id", _I, [_P]),
     ("zr_comm_create", _I, [_P, _I, _I, _I, C.POINTER(_P)]),
     ("zr_comm_destroy", None, [_P]),
+    ("zr_comm_size", _I, [_P, C.POINTER(_I)]),
     ("zr_comm_all_gather_async", _I, [_P, _P, _P, _SZ, _P]),
     ("zr_debug_glibc_math", _I, [_I, _P, _P, _P, _SZ, _P]),
     ("zr_cnn_estimate_device_views_async", _I, [_P, _P, _SZ, _P, _SZ, _F, _F, _P, _P]),
@@ -215,6 +219,11 @@ class Comm:
         with _StdoutToStderr():
             check(lib().zr_comm_create(buf, world, rank, device, C.byref(p)))
         self.ptr, self.world, self.rank = p.value, world, rank
+
+    def size(self) -> int:
+        n = C.c_int()
+        check(lib().zr_comm_size(self.ptr, C.byref(n)))
+        return n.value
 
     def all_gather_async(self, d_send: int, d_recv: int, nbytes: int, stream=None):
         check(lib().zr_comm_all_gather_async(self.ptr, d_send, d_recv, nbytes, stream))

@@ -67,7 +67,7 @@ LandmarkNetwork landmark_net(const std::string &name) {
 // Detector::detect_impl after inference on raw outputs (detection.rs:231-267)
 std::vector<Detection> detect_post(const std::string &net, py::array_t<float, py::array::c_style> boxes,
                                    py::array_t<float, py::array::c_style> logits, uint32_t img_w,
-                                   uint32_t img_h, float thresh, float iou) {
+                                   uint32_t img_h, float thresh, float iou, bool remove) {
     DetectorNetwork dn = detector_net(net);
     // network input sizes: short range 128, full range / palm 192 (the ONNX input shapes)
     const uint32_t s = dn.kind == NetworkKind::FaceDetectionShortRange ? 128 : 192;
@@ -77,6 +77,7 @@ std::vector<Detection> detect_post(const std::string &net, py::array_t<float, py
     dn.extract(boxes.data(), logits.data(), thresh, s, s, raw);
     NonMaxSuppression nms;
     nms.set_iou_thresh(iou);
+    if (remove) nms.set_mode(SuppressionMode::Remove);
     auto out = nms.process(raw);
     Rect rect;
     letterbox_view(img_w, img_h, AspectRatio::of(s, s), &rect);
@@ -195,7 +196,23 @@ PYBIND11_MODULE(_zaru_host, m) {
 
     m.def("detect_post", &detect_post, py::arg("network"), py::arg("boxes"), py::arg("logits"),
           py::arg("img_w"), py::arg("img_h"), py::arg("thresh") = Detector::DEFAULT_THRESHOLD,
-          py::arg("iou") = NonMaxSuppression::DEFAULT_IOU_THRESH);
+          py::arg("iou") = NonMaxSuppression::DEFAULT_IOU_THRESH, py::arg("remove") = false);
+    m.def("nms_ties", [](const std::string &net, py::array_t<float, py::array::c_style> logits, float thresh) {
+        // NonMaxSuppression::TieCount of a frame's candidates: (candidates, tied)
+        DetectorNetwork dn = detector_net(net);
+        if ((size_t)logits.size() != dn.anchors().size()) throw ZaruError(ZR_ERR_SHAPE, "one logit per anchor");
+        std::vector<Detection> raw;
+        for (size_t i = 0; i < dn.anchors().size(); i++) {
+            const float c = sigmoid(logits.data()[i]);
+            if (c < thresh) continue;
+            Detection d;
+            d.confidence = c;
+            raw.push_back(d);
+        }
+        NonMaxSuppression::TieCount t;
+        NonMaxSuppression().process(raw, &t);
+        return std::make_pair(t.candidates, t.tied);
+    }, py::arg("network"), py::arg("logits"), py::arg("thresh") = Detector::DEFAULT_THRESHOLD);
     m.def("anchors", [](const std::string &net) {
         auto a = detector_net(net).anchors();
         py::array_t<float> o({(py::ssize_t)a.size(), (py::ssize_t)2});
@@ -293,6 +310,8 @@ PYBIND11_MODULE(_zaru_host, m) {
         .def("set_redetect_interval", &DeviceHandTracker::set_redetect_interval, py::arg("ms"))
         .def("set_iou_thresh", &DeviceHandTracker::set_iou_thresh)
         .def("set_loss_threshold", &DeviceHandTracker::set_loss_threshold)
+        .def("set_palm_every_frame", &DeviceHandTracker::set_palm_every_frame, py::arg("on"))
+        .def("palm_frames", &DeviceHandTracker::palm_frames)
         .def("inject_detections", &DeviceHandTracker::inject_detections)
         .def("step", [](DeviceHandTracker &t, const std::vector<std::tuple<uint64_t, uint32_t, uint32_t, uint64_t>> &frames,
                         double now_ms) {
@@ -542,6 +561,9 @@ PYBIND11_MODULE(_zaru_host, m) {
             d["total_ms"] = t.total_ms;
             d["host_wait_ms"] = t.host_wait_ms;
             d["dropped_detections"] = t.dropped_detections;
+            d["nms_candidates"] = t.nms_candidates;
+            d["nms_tied"] = t.nms_tied;
+            d["nms_unpinned_frames"] = t.nms_unpinned_frames;
             d["frames"] = t.frames;
             d["detections"] = t.detections;
             d["rois"] = t.rois;

@@ -28,10 +28,20 @@ int32_t total_key(float f) {
 }  // namespace
 
 // nms.rs:59-145
-std::vector<Detection> NonMaxSuppression::process(std::vector<Detection> &dets) const {
+std::vector<Detection> NonMaxSuppression::process(std::vector<Detection> &dets, TieCount *ties) const {
     std::stable_sort(dets.begin(), dets.end(), [](const Detection &a, const Detection &b) {
         return total_key(a.confidence) < total_key(b.confidence);
     });
+    if (ties) {  // members of runs of equal keys in the sorted list
+        ties->candidates = (int)dets.size();
+        ties->tied = 0;
+        for (size_t i = 0; i < dets.size(); i++) {
+            const int32_t k = total_key(dets[i].confidence);
+            const bool eq = (i > 0 && total_key(dets[i - 1].confidence) == k) ||
+                            (i + 1 < dets.size() && total_key(dets[i + 1].confidence) == k);
+            ties->tied += eq ? 1 : 0;
+        }
+    }
     std::vector<Detection> out, group;
     while (!dets.empty()) {
         Detection seed = std::move(dets.back());

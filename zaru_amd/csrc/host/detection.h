@@ -36,7 +36,14 @@ class NonMaxSuppression {  // nms.rs:18-146
     SuppressionMode mode() const { return mode_; }
     // Sorts `dets` ascending by confidence (stable: ties keep input order, as Rust's
     // sort_unstable does for <= 20 elements) and returns the suppressed/averaged list.
-    std::vector<Detection> process(std::vector<Detection> &dets) const;
+    // `ties` (optional): the candidate count and how many of them share their confidence with
+    // another candidate.  Above 20 candidates Rust's sort_unstable (ipnsort) is not stable, so a
+    // frame with more than 20 candidates and a tie has an order the reference does not pin.
+    struct TieCount {
+        int candidates = 0, tied = 0;
+        bool unpinned() const { return candidates > 20 && tied > 0; }
+    };
+    std::vector<Detection> process(std::vector<Detection> &dets, TieCount *ties = nullptr) const;
 
   private:
     float iou_ = DEFAULT_IOU_THRESH;

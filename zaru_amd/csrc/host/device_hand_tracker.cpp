@@ -47,6 +47,10 @@ DeviceHandTracker::DeviceHandTracker(size_t streams, int slots, int device)
     views_.resize(nv);
     lm_out_.resize(nv * (size_t)hand_net_.num_landmarks * 3);
     nhands_.resize(n_);
+    due_.resize(n_);
+    due_views_.resize(n_);
+    ndue_.resize(1);
+    due_total_.resize(1);
     next_id_.resize(n_);
     next_det_.resize(n_);
     det_pending_.resize(n_);
@@ -72,6 +76,7 @@ DeviceHandTracker::DeviceHandTracker(size_t streams, int slots, int device)
     check(zr_memcpy_async(det_pending_.ptr, zi.data(), n_ * 4, 0, stream_));
     check(zr_memcpy_async(count_.ptr, zi.data(), n_ * 4, 0, stream_));
     check(zr_memcpy_async(dropped_.ptr, zi.data(), n_ * 4, 0, stream_));
+    check(zr_memcpy_async(due_total_.ptr, zl.data(), 8, 0, stream_));
     check(zr_stream_synchronize(stream_));  // the host vectors are pageable and go out of scope
     injected_.resize(n_);
 }
@@ -118,6 +123,8 @@ void DeviceHandTracker::step(const std::vector<Image> &frames, double now_ms) {
         check(zr_memcpy_async(lbox_.ptr, l.data(), l.size() * 4, 0, stream_));
         check(zr_memcpy_async(fsize_.ptr, fs.data(), fs.size() * 4, 0, stream_));
         check(zr_stream_synchronize(stream_));
+        const zr_view pv = to_zr_view(letterbox_view(W, H, palm_->aspect()));
+        check(zr_view_describe(&pv, 1, 0, &palm_tmpl_));
     }
     // injected detections replace the palm result this step consumes (test hook)
     bool any = false;
@@ -173,16 +180,35 @@ void DeviceHandTracker::step(const std::vector<Image> &frames, double now_ms) {
     float *outs[4] = {outs_[0].ptr, outs_[1].ptr, outs_[2].ptr, outs_[3].ptr};
     const ColorMapper hc = hand_->color_mapper();
     check(zr_cnn_estimate_device_views_async(hn.handle(), zf.data(), n_, views_.ptr, nv, hc.lo, hc.hi, outs, stream_));
-    // 4. BlazePalm on every frame (Detector::detect_impl, detection.rs:224-267), taken next step
-    std::vector<zr_view> pv(n_);
-    for (size_t i = 0; i < n_; i++) pv[i] = to_zr_view(letterbox_view(W, H, palm_->aspect()));
-    std::vector<uint32_t> pvf(n_);
-    for (size_t i = 0; i < n_; i++) pvf[i] = (uint32_t)i;
+    // 4. BlazePalm (Detector::detect_impl, detection.rs:224-267) on the streams step 2 asked to
+    // detect on, taken next step: their list and count stay on the device
     float *pd[2] = {palm_boxes_.ptr, palm_logits_.ptr};
-    palm_->estimate_async(std::vector<zr_frame>(zf.begin(), zf.end()), pv, pvf, pd, stream_);
-    check(zr_detect_post_async(palm_logits_.ptr, palm_boxes_.ptr, anchors_.ptr, lbox_.ptr, n_, &pcfg_, count_.ptr,
-                               dets_.ptr, dcap_, nullptr, 0, 0, 1, stream_));
+    if (palm_every_) {
+        std::vector<zr_view> pv(n_);
+        for (size_t i = 0; i < n_; i++) pv[i] = to_zr_view(letterbox_view(W, H, palm_->aspect()));
+        std::vector<uint32_t> pvf(n_);
+        for (size_t i = 0; i < n_; i++) pvf[i] = (uint32_t)i;
+        palm_->estimate_async(std::vector<zr_frame>(zf.begin(), zf.end()), pv, pvf, pd, stream_);
+        check(zr_detect_post_async(palm_logits_.ptr, palm_boxes_.ptr, anchors_.ptr, lbox_.ptr, n_, &pcfg_, count_.ptr,
+                                   dets_.ptr, dcap_, nullptr, 0, 0, 1, nullptr, stream_));
+        palm_frames_ += n_;
+    } else {
+        check(zr_due_compact_async(det_pending_.ptr, n_, &palm_tmpl_, due_.ptr, ndue_.ptr, due_views_.ptr, due_total_.ptr,
+                                   stream_));
+        const ColorMapper pc = palm_->color_mapper();
+        check(zr_cnn_estimate_device_views_count_async(palm_->nn().handle(), zf.data(), n_, due_views_.ptr, n_, ndue_.ptr,
+                                                       pc.lo, pc.hi, pd, stream_));
+        check(zr_detect_post_mapped_async(palm_logits_.ptr, palm_boxes_.ptr, anchors_.ptr, lbox_.ptr, n_, due_.ptr,
+                                          ndue_.ptr, &pcfg_, count_.ptr, dets_.ptr, dcap_, nullptr, stream_));
+    }
     steps_++;
+}
+
+uint64_t DeviceHandTracker::palm_frames() {
+    uint64_t due = 0;
+    check(zr_memcpy_async(&due, due_total_.ptr, 8, 1, stream_));
+    synchronize();
+    return palm_frames_ + due;
 }
 
 void DeviceHandTracker::synchronize() {

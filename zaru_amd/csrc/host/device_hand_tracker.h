@@ -6,8 +6,12 @@
 //      the hands' ROIs, start new hands, the swap_remove de-duplication, the redetection
 //      schedule (zr_hand_manage_async),
 //   3. the hand landmark network on every slot's view of this step's frame, and
-//   4. BlazePalm on every stream's frame with its device post-processing (zr_detect_post_async),
-//      whose detections step 2 consumes at the next step.
+//   4. BlazePalm with its device post-processing on the streams step 2 asked to detect on
+//      (tracking.rs:210-218: no hand tracked, or the redetection interval elapsed): step 2's
+//      request flags are compacted on the device into a stream list + count
+//      (zr_due_compact_async), the palm launches skip the images past that count
+//      (zr_cnn_estimate_device_views_count_async) and the post-processing writes each due stream's
+//      slot (zr_detect_post_mapped_async); step 2 consumes them at the next step.
 // The host enqueues only: no host round trip per frame.  Stream s owns `slots` hand slots.
 // Schedule: a palm detection requested at step t is taken at step t + 1 -- the host HandTracker's
 // schedule when every detection finishes within one frame (HandTracker::wait_detection before
@@ -31,6 +35,12 @@ class DeviceHandTracker {
     void set_redetect_interval(double ms) { cfg_.interval_ms = ms; }
     void set_iou_thresh(float t) { cfg_.iou_thresh = t; }
     void set_loss_threshold(float t) { tcfg_.loss_thresh = t; }
+    // A/B switch: BlazePalm on every stream's frame each step (the round-3 schedule; results of
+    // streams that did not ask are discarded) instead of on the due streams only
+    void set_palm_every_frame(bool on) { palm_every_ = on; }
+    // frames BlazePalm ran on so far (every_frame: all streams each step; else the due streams,
+    // counted from the device list after synchronize())
+    uint64_t palm_frames();
     // detections handed to stream s's next step as if its palm detection had produced them (test
     // hook, the host HandTracker's inject_detections); replaces that step's palm result
     void inject_detections(size_t s, const std::vector<Detection> &dets);
@@ -74,7 +84,12 @@ class DeviceHandTracker {
     DeviceArray<float> hroi_, lm_out_, outs_[4], palm_boxes_, palm_logits_, anchors_, lbox_, dets_;
     DeviceArray<int32_t> src_, nhands_, det_pending_, count_, dropped_;
     DeviceArray<double> next_det_;
-    DeviceArray<zr_view_desc> views_;
+    DeviceArray<zr_view_desc> views_, due_views_;
+    DeviceArray<int32_t> due_, ndue_;  // the due streams of a step and their count
+    zr_view_desc palm_tmpl_{};         // the letterboxed palm view (frame index set per stream)
+    bool palm_every_ = false;
+    uint64_t palm_frames_ = 0;         // every-frame mode
+    DeviceArray<uint64_t> due_total_;  // due streams summed over the steps (device)
     std::vector<std::vector<Detection>> injected_;
     std::vector<Rect> letterbox_;
 };

@@ -154,8 +154,15 @@ size_t DetectTrackPipeline::det_cap() const { return cfg_.det_cap; }
 void DetectTrackPipeline::enable_records(uint32_t rmax, uint32_t first_id, uint32_t id_stride, zr_comm *comm,
                                          int world) {
     if (!cfg_.device_post) throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "device records need device post-processing");
-    if (rmax == 0 || rmax > 64 || world < 1 || (comm && world < 1))
-        throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "bad record configuration");
+    if (rmax == 0 || rmax > 64 || world < 1) throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "bad record configuration");
+    if (comm) {
+        // the all-gather writes the communicator's nranks * bytes into a world-sized block
+        int nranks = 0;
+        check(zr_comm_size(comm, &nranks));
+        if (nranks != world)
+            throw ZaruError(ZR_ERR_INVALID_ARGUMENT, "world (" + std::to_string(world) + ") is not the communicator's rank count (" +
+                                                         std::to_string(nranks) + ")");
+    }
     if (gstream_) check(zr_stream_synchronize(gstream_));
     rec_rmax_ = rmax;
     rec_first_ = first_id;
@@ -358,7 +365,7 @@ void DetectTrackPipeline::stage_device_post(Slot &s, const std::vector<Image> &f
         s.inputs_ok = true;
     }
     Slot::Results &o = s.res[s.wr];
-    const size_t sum_bytes = 2 * nv * sizeof(zr_track_state) + n * sizeof(int32_t);
+    const size_t sum_bytes = 2 * nv * sizeof(zr_track_state) + 3 * n * sizeof(int32_t);  // + count, ties
     o.sum.resize(sum_bytes);
     o.h_sum.resize(sum_bytes);
     o.dets.resize(n * dcap * 20);
@@ -366,6 +373,7 @@ void DetectTrackPipeline::stage_device_post(Slot &s, const std::vector<Image> &f
     zr_track_state *d_state = reinterpret_cast<zr_track_state *>(o.sum.ptr);
     zr_track_state *d_seed = d_state + nv;
     int32_t *d_count = reinterpret_cast<int32_t *>(d_seed + nv);
+    int32_t *d_ties = d_count + n;
     s.d_views.resize(nv);
     zr_detpost_cfg pc{};
     pc.face = is_face_detector(cfg_.detector.kind) ? 1 : 0;
@@ -388,7 +396,7 @@ void DetectTrackPipeline::stage_device_post(Slot &s, const std::vector<Image> &f
     }
     check(zr_detect_post_async(s.d_logits.ptr, s.d_boxes.ptr, d_anchors_.ptr, s.d_lbox.ptr, n, &pc, d_count,
                                o.dets.ptr, dcap, rec, rec_rmax_, rec_first_ + (uint32_t)s.f0 * rec_stride_,
-                               rec_stride_, s.stream));
+                               rec_stride_, d_ties, s.stream));
     if (records) check(zr_event_record(s.ev_rec, s.stream));
     const zr_track_cfg tc = track_cfg();
     check(zr_track_seed_detections_async(d_count, o.dets.ptr, dcap, s.d_forced.ptr, s.d_nforced.ptr, s.d_fsize.ptr,
@@ -420,8 +428,9 @@ void DetectTrackPipeline::finish_device(Slot &s) {
     const Slot::Results &o = s.res[s.done];
     const size_t n = s.nf, R = std::max(1u, cfg_.max_rois_per_frame), nv = n * R;
     const zr_track_state *st = reinterpret_cast<const zr_track_state *>(o.h_sum.ptr);
-    const int32_t *cnt = reinterpret_cast<const int32_t *>(st + 2 * nv);
+    const int32_t *cnt = reinterpret_cast<const int32_t *>(st + 2 * nv), *tie = cnt + n;
     for (size_t i = 0; i < n; i++) {
+        add_ties(NonMaxSuppression::TieCount{tie[2 * i], tie[2 * i + 1]});
         times_.detections += (size_t)cnt[i];
         if ((size_t)cnt[i] > cfg_.det_cap) times_.dropped_detections += (size_t)cnt[i] - cfg_.det_cap;
     }
@@ -565,7 +574,7 @@ void DetectTrackPipeline::stage_decode_and_rois(Slot &s, const std::vector<Image
             }
         }
         auto &dets = dets_[s.f0 + i];
-        dets = nms_.process(raw);
+        dets = nms_.process(raw, &ties_[s.f0 + i]);
         map_detections(dets, s.letterbox[i], din_w);
     });
 
@@ -648,6 +657,7 @@ void DetectTrackPipeline::run(const std::vector<Image> &frames,
     times_ = StageTimes{};
     times_.frames = B;
     dets_.assign(B, {});
+    ties_.assign(B, {});
     rois_.clear();
     if (B == 0) return;
     // split into sub-batches (software pipeline): GPU det(k+1) overlaps host decode(k), GPU
@@ -697,6 +707,7 @@ void DetectTrackPipeline::run(const std::vector<Image> &frames,
     }
     times_.rois = rois_.size();
     for (auto &d : dets_) times_.detections += d.size();
+    for (const auto &t : ties_) add_ties(t);
     for (auto &r : rois_) times_.tracked += r.tracked ? 1 : 0;
     times_.total_ms = ms_since(t0);
 }
@@ -728,6 +739,7 @@ void DetectTrackPipeline::step(bool more) {
     const size_t B = frames.size(), S = active_slots_;
     if (S == 0) return;
     dets_.assign(B, {});
+    ties_.assign(B, {});
     rois_.clear();
     // device mode: a slot's whole step is on its stream; take its results and enqueue its next
     // step at once, while the other slots' steps run
@@ -774,6 +786,7 @@ void DetectTrackPipeline::step(bool more) {
     times_.frames += B;
     times_.rois += rois_.size();
     for (auto &d : dets_) times_.detections += d.size();
+    for (const auto &t : ties_) add_ties(t);
     for (auto &r : rois_) times_.tracked += r.tracked ? 1 : 0;
     times_.total_ms = ms_since(steps_t0_);
 }

@@ -60,6 +60,10 @@ struct StageTimes {
     // detections past PipelineConfig::det_cap (device mode; 0 with the default cap, which keeps
     // the detector's whole output)
     size_t dropped_detections = 0;
+    // NMS candidates (conf >= threshold), those sharing their exact confidence with another, and
+    // frames with > 20 candidates and a tie: the reference's sort_unstable order is not pinned
+    // there (nms.rs:66), this build's is anchor order
+    size_t nms_candidates = 0, nms_tied = 0, nms_unpinned_frames = 0;
 };
 
 struct PipelineConfig {
@@ -214,6 +218,12 @@ class DetectTrackPipeline {
     void *stream_ = nullptr;
     std::vector<std::unique_ptr<Slot>> slots_;
     mutable std::vector<std::vector<Detection>> dets_;
+    std::vector<NonMaxSuppression::TieCount> ties_;  // host mode: per frame of the step
+    void add_ties(const NonMaxSuppression::TieCount &t) {
+        times_.nms_candidates += (size_t)t.candidates;
+        times_.nms_tied += (size_t)t.tied;
+        times_.nms_unpinned_frames += t.unpinned() ? 1 : 0;
+    }
     mutable std::vector<RoiResult> rois_;
     mutable bool stale_ = false;  // device mode: dets_ / rois_ not yet built from the last step
     StageTimes times_;

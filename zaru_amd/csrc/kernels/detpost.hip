@@ -8,7 +8,10 @@
 //     contraction: -ffp-contract=off), the angle with glibc's atan2f;
 //   * the NMS order is ascending total_cmp of the confidence, ties in anchor order (the host's
 //     stable sort, = Rust's sort_unstable on <= 20 elements), seeds popped from the top, each
-//     group summed seed first then in ascending order.
+//     group summed seed first then in ascending order.  Above 20 candidates Rust sorts with
+//     ipnsort, which is not stable: a frame with more than 20 candidates and an exact confidence
+//     tie (sigmoid saturates to 1.0f above logit ~16.6) has an order the reference does not pin;
+//     `ties` reports each frame's candidate and tied-candidate counts so callers can count them.
 // Candidates (anchor, conf) and their rects live in LDS; the group sums re-decode a member's
 // keypoints from the raw outputs, which is the same arithmetic as decoding it once.
 #include "../runtime/zr_track.h"
@@ -51,6 +54,8 @@ __device__ __forceinline__ Decoded decode(const DetPostParams &P, const float *b
 __global__ __launch_bounds__(64) void det_post_kernel(const DetPostParams P) {
     extern __shared__ float lds_dp[];
     const int f = blockIdx.x, lane = threadIdx.x;
+    if (P.nact && f >= *P.nact) return;  // (whole wave)
+    const int fo = P.map ? P.map[f] : f;  // the output slot
     const int A = P.A;
     int *ca = (int *)lds_dp;               // candidate anchors, anchor order    [A]
     float *cc = lds_dp + A;                // their confidences                  [A]
@@ -80,6 +85,9 @@ __global__ __launch_bounds__(64) void det_post_kernel(const DetPostParams P) {
     }
     __syncthreads();
     // 2. rects, and 3. the ascending stable order: rank = #smaller keys + #equal keys before
+    __shared__ int s_tied;  // candidates whose key another candidate shares (NonMaxSuppression::TieCount)
+    if (lane == 0) s_tied = 0;
+    __syncthreads();
     for (int i = lane; i < n; i += 64) {
         const float *b = boxes + (int64_t)ca[i] * P.D;
         cr[4 * i] = b[0] + P.anchors[2 * ca[i]] * (float)P.in_w;
@@ -87,22 +95,24 @@ __global__ __launch_bounds__(64) void det_post_kernel(const DetPostParams P) {
         cr[4 * i + 2] = b[2];
         cr[4 * i + 3] = b[3];
         const int32_t ki = total_key(cc[i]);
-        int r = 0;
+        int r = 0, eq = 0;
         for (int j = 0; j < n; ++j) {
             const int32_t kj = total_key(cc[j]);
             r += (kj < ki || (kj == ki && j < i)) ? 1 : 0;
+            eq += (kj == ki && j != i) ? 1 : 0;
         }
         ord[r] = i;
+        if (eq) atomicAdd(&s_tied, 1);
     }
     __syncthreads();
 
     // 4. NMS: pop the most confident, group everything within the IoU threshold (keeping order),
     // average the group weighted by confidence, map into the frame
-    const float *lb = P.letterbox + 4 * f;
+    const float *lb = P.letterbox + 4 * fo;
     const float scale = lb[2] / (float)P.in_w;
     const float tlx = lb[0] - lb[2] * 0.5f, tly = lb[1] - lb[3] * 0.5f;
     const int rw = 2 + 20 * P.rmax;
-    float *rec = P.rec ? P.rec + (int64_t)f * rw : nullptr;
+    float *rec = P.rec ? P.rec + (int64_t)fo * rw : nullptr;
     int rem = n, out = 0;
     while (rem > 0) {
         const int seed = ord[--rem];
@@ -146,7 +156,7 @@ __global__ __launch_bounds__(64) void det_post_kernel(const DetPostParams P) {
                 e[7 + 2 * k] = k < P.nkp ? (b[5 + 2 * k] + cyi) * scale + tly : 0.f;
             }
             if (out < P.dcap) {
-                float *o = P.dets + ((int64_t)f * P.dcap + out) * 20;
+                float *o = P.dets + ((int64_t)fo * P.dcap + out) * 20;
 #pragma unroll
                 for (int k = 0; k < 20; ++k) o[k] = e[k];
             }
@@ -201,7 +211,7 @@ __global__ __launch_bounds__(64) void det_post_kernel(const DetPostParams P) {
                 e[7 + 2 * k] = k < P.nkp ? ky[k] * scale + tly : 0.f;
             }
             if (out < P.dcap) {
-                float *o = P.dets + ((int64_t)f * P.dcap + out) * 20;
+                float *o = P.dets + ((int64_t)fo * P.dcap + out) * 20;
 #pragma unroll
                 for (int k = 0; k < 20; ++k) o[k] = e[k];
             }
@@ -213,9 +223,13 @@ __global__ __launch_bounds__(64) void det_post_kernel(const DetPostParams P) {
         ++out;
     }
     if (lane == 0) {
-        P.count[f] = out;
+        P.count[fo] = out;
+        if (P.ties) {
+            P.ties[2 * fo] = n;
+            P.ties[2 * fo + 1] = s_tied;
+        }
         if (rec) {
-            const uint32_t id = P.first_id + (uint32_t)f * P.id_stride;
+            const uint32_t id = P.first_id + (uint32_t)fo * P.id_stride;
             rec[0] = __builtin_bit_cast(float, id);
             rec[1] = __builtin_bit_cast(float, (uint32_t)out);
             for (int k = 20 * min(out, P.rmax); k < 20 * P.rmax; ++k) rec[2 + k] = 0.f;

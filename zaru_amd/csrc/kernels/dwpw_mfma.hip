@@ -62,6 +62,7 @@ __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) 
     const int kh = lane >> 5, col = lane & 31;
     const int wm = wave % WM, wn = wave / WM;
     const int j0 = tile * BN, m0 = blockIdx.y * BM;
+    if (G.nact && j0 >= *G.nact * G.P) return;  // images past the device count
     const int Cin = G.K;
 
     // depthwise role: column dj of the tile, channels dc, dc + CPAR, ... of each chunk
@@ -257,7 +258,15 @@ __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) 
 // occupancy.  With MTW = 2 the two register sets would cost a wave per SIMD, so
 // those layouts stage the weights' chunk rows in the DMA buffer.
 // (MTW == 1: 4 waves per SIMD fit in 128 registers without spills)
-template <int K, int S, int WM, int MTW, int DFKC>
+// RT > 0 (form "rt"): the depthwise runs as row tasks instead of one tap read per output and tap.
+// A task is RT adjacent outputs of one output row of one channel; it reads each of its K input
+// rows once as a window of (RT - 1) * S + K floats with 8-byte LDS reads (RT * K FMAs per row for
+// ceil(window / 2) reads, where the per-output form issues K reads per row per output), keeps the
+// channel's K^2 weights in registers for its NRT tasks, and masks the padding statically: a row
+// outside the image reads a zeroed LDS block, the first / last segment of a row zeroes its PL / PR
+// window floats.  The arithmetic is the per-output form's: bias + fmaf over the taps in (ky, kx)
+// order, masked taps as fmaf(w, 0, a) -- so the bits are too (tests/test_gpu_forms.py, -rt).
+template <int K, int S, int WM, int MTW, int DFKC, int RT>
 __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int runmax, int bufsz, int bx, int by, int gx) {
     constexpr int WN = 4 / WM, BN = WN * 32, BM = WM * MTW * 32, KK = K * K;
     constexpr int CPAR = 256 / BN, PER = DFKC / CPAR;
@@ -277,6 +286,7 @@ __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int 
     const int kh = lane >> 5, col = lane & 31;
     const int wm = wave % WM, wn = wave / WM;
     const int j0 = tile * BN, m0 = by * BM;
+    if (G.nact && j0 >= *G.nact * G.P) return;  // images past the device count
     const int Cin = G.K, H = P.in.H, W = P.in.W, Pin = H * W, OW = P.OW, Pq = G.P;
     const int pt = P.pad_t, pl = P.pad_l;
 
@@ -353,6 +363,41 @@ __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int 
             mask |= (iy >= 0 && iy < H && ix >= 0 && ix < W ? 1u : 0u) << (ky * K + kx);
         }
 
+    // row-task geometry (RT > 0): thread tid runs tasks tid * NRT + r of a chunk, all of one
+    // channel (SEGS % NRT == 0); per task the run index of its aligned window start in row ky = 0,
+    // the rows inside the image, and whether it is the first / last segment of its output row
+    constexpr int RTE = RT > 0 ? RT : 1;
+    constexpr int PLx = DwPad<K, S>::L, OFF = PLx & 1;
+    constexpr int WW = (RTE - 1) * S + K, PR = WW - RTE * S - PLx;  // window floats, right pad
+    constexpr int NB64 = (OFF + WW + 1) / 2;                        // 8-byte reads per window row
+    constexpr int SEGS = BN / RTE, TASKS = DFKC * SEGS, NRT = TASKS > 256 ? TASKS / 256 : 1;
+    static_assert(RT == 0 || (RT % 2 == 0 && BN % RT == 0 && SEGS % NRT == 0 && (TASKS <= 256 || TASKS % 256 == 0)),
+                  "row-task layout");
+    const int rt_c = RT > 0 ? tid * NRT / SEGS : 0;
+    const bool rt_on = RT > 0 && tid * NRT < TASKS;
+    int rt_base[NRT];
+    uint32_t rt_vm[NRT];
+    bool rt_first[NRT], rt_last[NRT], rt_ok[NRT];
+    if constexpr (RT > 0) {
+        if (tid < 16) reinterpret_cast<float4 *>(lds_all)[tid] = make_float4(0.f, 0.f, 0.f, 0.f);  // the zero rows
+#pragma unroll
+        for (int r = 0; r < NRT; ++r) {
+            const int g = (tid * NRT + r) % SEGS;
+            const int j = j0 + g * RT;
+            rt_ok[r] = rt_on && j < G.ncols;
+            const int jj = rt_ok[r] ? j : 0;
+            const int tn = jj / Pq, tq = jj - tn * Pq, toy = tq / OW, tox = tq - toy * OW;
+            const int iy0 = toy * S - pt;
+            rt_base[r] = tn * Pin + iy0 * W + tox * S - PLx - OFF - s0;
+            uint32_t vm = 0;
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky) vm |= (iy0 + ky >= 0 && iy0 + ky < H ? 1u : 0u) << ky;
+            rt_vm[r] = vm;
+            rt_first[r] = tox == 0;
+            rt_last[r] = tox + RT == OW;
+        }
+    }
+
     f32x16 acc[MTW];
 #pragma unroll
     for (int t = 0; t < MTW; ++t)
@@ -370,6 +415,49 @@ __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int 
             wload(kc + DFKC, wnx);
         }
         const float *sIn = buf, *sW = buf + DFKC * runmax, *sDW = sW + (WREG ? 0 : DFKC * BM), *sDB = sDW + KKP;
+        if constexpr (RT > 0) {
+            if (rt_on) {
+                const int c = rt_c;
+                float wr[KK];
+#pragma unroll
+                for (int t = 0; t < KK; ++t) wr[t] = sDW[c * KK + t];
+                const float bb = sDB[c];
+                const bool live = kc + c < Cin;
+                const float *chan = sIn + c * runmax;
+#pragma unroll
+                for (int r = 0; r < NRT; ++r) {
+                    float a[RTE];
+#pragma unroll
+                    for (int o = 0; o < RTE; ++o) a[o] = bb;
+#pragma unroll
+                    for (int ky = 0; ky < K; ++ky) {
+                        const float *row = ((rt_vm[r] >> ky) & 1u) ? chan + rt_base[r] + ky * W : lds_all;
+                        float x[2 * NB64];
+#pragma unroll
+                        for (int e = 0; e < NB64; ++e) {
+                            const float2 v = *reinterpret_cast<const float2 *>(row + 2 * e);
+                            x[2 * e] = v.x;
+                            x[2 * e + 1] = v.y;
+                        }
+#pragma unroll
+                        for (int e = 0; e < PLx; ++e) x[OFF + e] = rt_first[r] ? 0.f : x[OFF + e];
+#pragma unroll
+                        for (int e = WW - PR; e < WW; ++e) x[OFF + e] = rt_last[r] ? 0.f : x[OFF + e];
+#pragma unroll
+                        for (int kx = 0; kx < K; ++kx)
+#pragma unroll
+                            for (int o = 0; o < RTE; ++o) a[o] = __builtin_fmaf(wr[ky * K + kx], x[OFF + o * S + kx], a[o]);
+                    }
+                    apply_act_n<RTE>(P.dw_act, a, [&](int) { return live ? kc + c : Cin - 1; });
+                    const int g = (tid * NRT + r) % SEGS;
+                    float *dst = sD + c * BN + g * RTE;
+#pragma unroll
+                    for (int o = 0; o < RTE; o += 2)
+                        *reinterpret_cast<float2 *>(dst + o) =
+                            make_float2(live && rt_ok[r] ? a[o] : 0.f, live && rt_ok[r] ? a[o + 1] : 0.f);
+                }
+            }
+        } else {
         float dv[PER];
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
@@ -393,6 +481,7 @@ __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int 
         });
 #pragma unroll
         for (int i = 0; i < PER; ++i) sD[(dc + CPAR * i) * BN + dj] = kc + dc + CPAR * i < Cin ? dv[i] : 0.f;
+        }
         // publish sD without draining the next chunk's DMA and weight loads (a __syncthreads
         // would wait vmcnt(0))
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -422,18 +511,18 @@ __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int 
     for (int t = 0; t < MTW; ++t) epilogue_tile(G, acc[t], on, oq, m0 + (wm * MTW + t) * 32, kh);
 }
 
-template <int K, int S, int WM, int MTW, int DFKC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTW == 1 ? 4 : 1)))
+template <int K, int S, int WM, int MTW, int DFKC, int RT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTW == 1 ? 4 : RT > 0 ? 2 : 1)))
 void dwpw_dma_kernel(const DwPwParams P, int nct, int runmax, int bufsz) {
-    dwpw_dma_body<K, S, WM, MTW, DFKC>(P, nct, runmax, bufsz, blockIdx.x, blockIdx.y, gridDim.x);
+    dwpw_dma_body<K, S, WM, MTW, DFKC, RT>(P, nct, runmax, bufsz, blockIdx.x, blockIdx.y, gridDim.x);
 }
 
 // sibling layers in one launch (group.h): a0 = nct, a1 = runmax, a2 = bufsz of each part
-template <int K, int S, int WM, int MTW, int DFKC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTW == 1 ? 4 : 1)))
+template <int K, int S, int WM, int MTW, int DFKC, int RT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTW == 1 ? 4 : RT > 0 ? 2 : 1)))
 void dwpw_dma_group_kernel(const LaunchGroup<DwPwParams> G) {
     const GroupSlot t = group_slot(G);
-    dwpw_dma_body<K, S, WM, MTW, DFKC>(G.p[t.g], G.a0[t.g], G.a1[t.g], G.a2[t.g], t.bx, t.by, G.gx[t.g]);
+    dwpw_dma_body<K, S, WM, MTW, DFKC, RT>(G.p[t.g], G.a0[t.g], G.a1[t.g], G.a2[t.g], t.bx, t.by, G.gx[t.g]);
 }
 
 namespace {
@@ -502,6 +591,41 @@ static int dfkc_for(int wgs, int cin) {
     return wgs < 512 && cin >= 64 ? 32 : 16;  // (32 channels in one chunk measured slower: 12.9 -> 15.2 us)
 }
 
+// Outputs per row task of the DMA form (0: the per-output depthwise).  R_hi = DFKC * BN / 256 keeps
+// every thread busy with one task per NRT; R_hi / 2 when the output width does not split into R_hi
+// segments.  Needs the models' TF-style padding with W = OW * S (so a row's first / last segment
+// holds all of its padding) and an even R (8-byte aligned windows: even W and run starts).
+// the widest row task an instance is built for: DFKC * BN / 256, capped where the window and the
+// K^2 weights would cost occupancy next to the accumulators (5x5 at MTW = 1 and MTW >= 3: 2, else 8)
+constexpr int rt_hi(int K, int MTW, int r) {
+    return r < 2 ? 2 : (MTW == 1 && K == 5) || MTW >= 3 ? 2 : r > 8 ? 8 : r;
+}
+
+template <int K, int S>
+static int rt_for(const DwPwParams &p, int bn, int r_hi) {
+    if (!form_on(FORM_RT) || p.pad_l != DwPad<K, S>::L || p.pad_t != DwPad<K, S>::L || p.in.W != p.OW * S) return 0;
+    for (int r = r_hi; r >= 2 && r >= r_hi / 2; r /= 2)
+        if (p.OW % r == 0 && bn % r == 0) return r;
+    return 0;
+}
+
+template <int K, int S, int WM, int MTW, int DFKC>
+static const char *dma_launch(const DwPwParams &p, dim3 grid, size_t lds, int nct, int runmax, int bufsz, hipStream_t s) {
+    constexpr int BN = (4 / WM) * 32, RH = rt_hi(K, MTW, DFKC * BN / 256);
+    const int rt = rt_for<K, S>(p, BN, RH);
+    if (rt == RH) {
+        hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, DFKC, RH>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
+        return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,%d,%d>", K, S, WM, MTW, DFKC, RH);
+    }
+    if constexpr (RH >= 4)
+        if (rt == RH / 2) {
+            hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, DFKC, RH / 2>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
+            return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,%d,%d>", K, S, WM, MTW, DFKC, RH / 2);
+        }
+    hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, DFKC, 0>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
+    return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,%d,0>", K, S, WM, MTW, DFKC);
+}
+
 template <int K, int S, int WM, int MTW>
 const char *dwpw_go(const DwPwParams &p, hipStream_t s) {
     constexpr int BN = (4 / WM) * 32, BM = WM * MTW * 32;
@@ -514,20 +638,14 @@ const char *dwpw_go(const DwPwParams &p, hipStream_t s) {
         // of a few dozen workgroups are nothing but those round trips)
         const int dk = dfkc_for(nct * mb, p.g.K);
         if (dk >= 64)
-            if (const size_t lds = dma_plan<K, S, WM, MTW, 64>(p, &runmax, &bufsz)) {
-                hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, 64>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
-                return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,64>", K, S, WM, MTW);
-            }
+            if (const size_t lds = dma_plan<K, S, WM, MTW, 64>(p, &runmax, &bufsz))
+                return dma_launch<K, S, WM, MTW, 64>(p, grid, lds, nct, runmax, bufsz, s);
         if (dk >= 32)
-            if (const size_t lds = dma_plan<K, S, WM, MTW, 32>(p, &runmax, &bufsz)) {
-                hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, 32>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
-                return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,32>", K, S, WM, MTW);
-            }
+            if (const size_t lds = dma_plan<K, S, WM, MTW, 32>(p, &runmax, &bufsz))
+                return dma_launch<K, S, WM, MTW, 32>(p, grid, lds, nct, runmax, bufsz, s);
     }
-    if (const size_t lds = dma_plan<K, S, WM, MTW, 16>(p, &runmax, &bufsz)) {
-        hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, 16>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
-        return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,16>", K, S, WM, MTW);
-    }
+    if (const size_t lds = dma_plan<K, S, WM, MTW, 16>(p, &runmax, &bufsz))
+        return dma_launch<K, S, WM, MTW, 16>(p, grid, lds, nct, runmax, bufsz, s);
     const bool v4 = v4_ok(p);
     if (v4) hipLaunchKernelGGL((dwpw_kernel<K, S, WM, MTW, 1, true>), grid, dim3(256), 0, s, p, nct);
     else hipLaunchKernelGGL((dwpw_kernel<K, S, WM, MTW, 1, false>), grid, dim3(256), 0, s, p, nct);
@@ -607,7 +725,11 @@ namespace {
 
 template <int K, int S, int WM, int MTW, int DFKC>
 const char *dma_group(const DwPwParams *p, int n, hipStream_t s) {
-    constexpr int BN = (4 / WM) * 32, BM = WM * MTW * 32;
+    constexpr int BN = (4 / WM) * 32, BM = WM * MTW * 32, RH = rt_hi(K, MTW, DFKC * BN / 256);
+    // one row-task width for every part (the parts are siblings of one shape)
+    const int rt = rt_for<K, S>(p[0], BN, RH);
+    for (int i = 1; i < n; ++i)
+        if (rt_for<K, S>(p[i], BN, RH) != rt) return nullptr;
     LaunchGroup<DwPwParams> G{};
     G.n = n;
     size_t lds = 0;
@@ -625,8 +747,17 @@ const char *dma_group(const DwPwParams *p, int n, hipStream_t s) {
         total += G.gx[i] * mb;
     }
     for (int i = n; i <= ZR_GROUP_MAX; ++i) G.start[i] = total;
-    hipLaunchKernelGGL((dwpw_dma_group_kernel<K, S, WM, MTW, DFKC>), dim3(total), dim3(256), lds, s, G);
-    return kernel_name("dwpw_dma_group_kernel<%d,%d,%d,%d,%d>", K, S, WM, MTW, DFKC);
+    if (rt == RH) {
+        hipLaunchKernelGGL((dwpw_dma_group_kernel<K, S, WM, MTW, DFKC, RH>), dim3(total), dim3(256), lds, s, G);
+        return kernel_name("dwpw_dma_group_kernel<%d,%d,%d,%d,%d,%d>", K, S, WM, MTW, DFKC, RH);
+    }
+    if constexpr (RH >= 4)
+        if (rt == RH / 2) {
+            hipLaunchKernelGGL((dwpw_dma_group_kernel<K, S, WM, MTW, DFKC, RH / 2>), dim3(total), dim3(256), lds, s, G);
+            return kernel_name("dwpw_dma_group_kernel<%d,%d,%d,%d,%d,%d>", K, S, WM, MTW, DFKC, RH / 2);
+        }
+    hipLaunchKernelGGL((dwpw_dma_group_kernel<K, S, WM, MTW, DFKC, 0>), dim3(total), dim3(256), lds, s, G);
+    return kernel_name("dwpw_dma_group_kernel<%d,%d,%d,%d,%d,0>", K, S, WM, MTW, DFKC);
 }
 
 template <int K, int S, int DFKC>

@@ -33,6 +33,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const StemParams P) {
     const int tiles_x = (P.OW + STW - 1) / STW;
     const int ty0 = (blockIdx.x / tiles_x) * STH, tx0 = (blockIdx.x % tiles_x) * STW;
     const int n = blockIdx.y;
+    if (P.nact && n >= *P.nact) return;  // (whole workgroup, before any barrier)
     const int iy0 = ty0 * S - P.pad_t, ix0 = tx0 * S - P.pad_l;
     if constexpr (PRE) {
         // all of this thread's pixel gathers are issued before the first is used
@@ -156,6 +157,7 @@ __global__ __launch_bounds__(256) void dwpw_valu_kernel(const DwPwParams P, int 
     if (tile >= ntiles) return;  // whole workgroup, before any barrier
     const int tid = threadIdx.x;
     const int n = tile / tpi, q0 = (tile - n * tpi) * VTQ;
+    if (G.nact && n >= *G.nact) return;
     const int Pq = G.P, H = P.in.H, W = P.in.W, Cin = G.K, OW = P.OW;
     const int oy_a = q0 / OW, oy_b = min(q0 + VTQ - 1, Pq - 1) / OW;
     const int iy_a = oy_a * S - P.pad_t;
@@ -329,6 +331,7 @@ __global__ __launch_bounds__(256) void dwpw_vres_kernel(const DwPwParams P, int 
     if (tile >= ntiles) return;  // whole workgroup, before any barrier
     const int tid = threadIdx.x;
     const int n = tile / tpi, q0 = (tile - n * tpi) * VT;
+    if (G.nact && n >= *G.nact) return;
     const int Pq = G.P, H = P.in.H, W = P.in.W, Cin = G.K, OW = P.OW, r_C = G.r_C;
     const int oy_a = q0 / OW, oy_b = min(q0 + VT - 1, Pq - 1) / OW;
     const int iy_a = oy_a * S - P.pad_t;

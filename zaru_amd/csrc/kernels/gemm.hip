@@ -32,6 +32,7 @@ __device__ __forceinline__ void gemm_body(const GemmParams &P, int bx, int by) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int kh = lane >> 5, col = lane & 31;
     const int m0 = by * (MT * 32);
+    if (P.nact && bx * 128 >= *P.nact * P.P) return;  // (whole workgroup) images past the device count
     const int j = (bx * 4 + wave) * 32 + col;
     const bool valid = j < P.ncols;
     const int jj = valid ? j : 0;
@@ -183,6 +184,7 @@ __device__ __forceinline__ void gemm_tiled_body(const GemmParams &P, int mblocks
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int kh = lane >> 5, col = lane & 31;
     const int j0 = ct * BN, m0 = mb * MR;
+    if (P.nact && j0 >= *P.nact * P.P) return;  // images past the device count
     const int nchunks = (P.K + TKC - 1) / TKC;
 
     float4 rx[XV], rw[WV];
@@ -424,8 +426,15 @@ struct GemmChoice {
 static GemmChoice choose_gemm(const GemmParams &p) {
     GemmChoice c{};
     const int mtiles = p.Mpad / 32;
-    // LDS-tiled path: X must be a row-major [K][ncols] matrix with 16-B aligned rows
-    const bool rowmajor = p.KK == 1 && p.x_sN == p.P && (p.x_sC % 4) == 0 && (p.ncols % 4) == 0 &&
+    // LDS-tiled path: X must be a row-major [K][ncols] matrix with 16-B aligned rows.  A row whose
+    // length is not a multiple of 4 (N x 7^2 or N x 3^2 columns for odd N) is read in whole float4s
+    // up to round_up(ncols, 4): the arena pads every channel plane to whole groups of 4 images
+    // (Binding::Ns), so the slack is inside the row; its columns are computed and never stored.
+    // (K <= 128 single-tile 1x1s over such rows keep the small-K form: the FaceMesh 3^2 tail.)
+    const int nch_k = (p.Kpad + KC - 1) / KC;
+    const bool tail_ok = (p.ncols % 4) == 0 ||
+                         (p.x_sC >= (int64_t)(p.ncols + 3) / 4 * 4 && !(mtiles == 1 && nch_k <= 4 && form_on(FORM_ROWS)));
+    const bool rowmajor = p.KK == 1 && p.x_sN == p.P && (p.x_sC % 4) == 0 && tail_ok &&
                           ((uintptr_t)p.x % 16) == 0 && (p.Mpad % 4) == 0 && ((uintptr_t)p.wt % 16) == 0;
     if (rowmajor) {
         // K <= 64 (the expand convs): one or two K-chunks, so operand reuse buys nothing and

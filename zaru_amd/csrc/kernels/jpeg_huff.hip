@@ -43,10 +43,11 @@ __global__ __launch_bounds__(JH_LANES) void jpeg_huff_kernel(const JpegHuffParam
     int pred[3] = {0, 0, 0};
     bool bad = false;
     const int m0 = iv * F.restart, m1 = min(m0 + F.restart, F.nmcu);
-    // Every block of the interval is written, also after a corrupt symbol: from the first bad
-    // code on, the rest of the interval gets all-zero blocks (libjpeg's insufficient-data rule:
-    // jdhuff.c zeroes the MCU and skips decoding), so no block keeps a previous frame's
-    // coefficients from the reused buffer.  The frame's error flag reports it.
+    // Every block of the interval is written, also after a corrupt symbol: the block holding the
+    // first bad code and the rest of the interval are all-zero blocks (libjpeg's insufficient-data
+    // rule: jdhuff.c zeroes the MCU and skips decoding; the sync decoder's rule per frame), so no
+    // block keeps a partial decode or a previous frame's coefficients from the reused buffer.  The
+    // frame's error flag reports it.
     for (int m = m0; m < m1; m++) {
         const int my = m / F.mcux, mx = m - my * F.mcux;
         for (int c = 0; c < F.ncomp; c++) {
@@ -97,8 +98,9 @@ __global__ __launch_bounds__(JH_LANES) void jpeg_huff_kernel(const JpegHuffParam
                         k = bad_now ? 64 : coef ? kn + 1 : r == 15 ? k + 16 : 64;
                         bad |= bad_now;
                     }
+                    const int4 zero4 = make_int4(0, 0, 0, 0);
 #pragma unroll
-                    for (int z = 0; z < 8; z++) b4[z] = mine[z];
+                    for (int z = 0; z < 8; z++) b4[z] = bad ? zero4 : mine[z];  // (the bad block too)
                 }
         }
     }

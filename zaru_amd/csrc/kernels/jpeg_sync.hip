@@ -200,9 +200,12 @@ __global__ __launch_bounds__(256) void jpeg_sync_scan_kernel(const JpegSyncParam
 }
 
 // Per frame: the lanes' first block indices and DC predictors (an exclusive scan of their block
-// counts and DC sums), in chunks of 256 lanes.  A lane whose start is not its predecessor's exit
-// (the sync passes ran out) or that follows a bad code ends the frame's decodable part:
-// err_block = the first block not decoded, and the frame's error flag is set.
+// counts and DC sums), in chunks of 256 lanes.  The first lane that fails ends the lanes' part:
+//   * a bad code on the true trajectory (corrupt data): err_block = that block, the frame's error
+//     flag is set, and the zero pass clears every block from it on;
+//   * a start that is not its predecessor's exit (the sync passes ran out before that lane fell
+//     into step -- a valid scan): no flag; err_block[1] = the lane, err_block[2] = its first block,
+//     and jpeg_sync_serial_kernel decodes the rest of the frame from its predecessor's exit.
 __global__ __launch_bounds__(256) void jpeg_sync_prefix_kernel(const JpegSyncParams P) {
     const JpegSyncFrame &F = P.frames[blockIdx.x];
     const JpegSyncState *x = F.x;
@@ -211,6 +214,8 @@ __global__ __launch_bounds__(256) void jpeg_sync_prefix_kernel(const JpegSyncPar
     int carry[4] = {0, 0, 0, 0};
     bool dead = false;
     int err_block = F.nblocks;
+    __shared__ int s_sync_lane, s_sync_blk;  // the first out-of-step lane (-1: none) and its block
+    if (threadIdx.x == 0) s_sync_lane = -1;
     for (int c0 = 0; c0 < F.nseg; c0 += 256) {  // (after a failure: every later lane base = -1)
         const int t = threadIdx.x, s = c0 + t;
         int v[4] = {0, 0, 0, 0};
@@ -259,7 +264,14 @@ __global__ __launch_bounds__(256) void jpeg_sync_prefix_kernel(const JpegSyncPar
             F.pred[3 * s] = ex[1];
             F.pred[3 * s + 1] = ex[2];
             F.pred[3 * s + 2] = ex[3];
-            if (s == fs) err_block = fail_at;  // (only lane fs's thread holds it)
+            if (s == fs) {  // (only lane fs's thread holds it)
+                if (bad_start) {
+                    s_sync_lane = s;
+                    s_sync_blk = fail_at;
+                } else {
+                    err_block = fail_at;
+                }
+            }
         }
         for (int k = 0; k < 4; ++k) carry[k] += sc[k][255];
         dead = dead || fs < (1 << 30);
@@ -277,7 +289,57 @@ __global__ __launch_bounds__(256) void jpeg_sync_prefix_kernel(const JpegSyncPar
     __syncthreads();
     if (threadIdx.x == 0) {
         F.err_block[0] = s_err;
+        F.err_block[1] = s_sync_lane;
+        F.err_block[2] = s_sync_blk;
         if (s_err < F.nblocks) P.error[F.frame] = 1;
+    }
+}
+
+// The rest of a frame whose sync passes ran out (err_block[1] = the first lane out of step):
+// decoded serially by one lane from the predecessor's exit -- the true state there, since every
+// earlier lane is in step -- with the predictors and block index the prefix gave that lane.  Only
+// a bad code here is corrupt data (err_block[0] and the flag, then the zero pass).  This is the
+// rare path (a long chain of out-of-step lanes in a dense scan): correct, one symbol chain long.
+__global__ __launch_bounds__(64) void jpeg_sync_serial_kernel(const JpegSyncParams P) {
+    __shared__ JpegHuffTable T[8];
+    __shared__ uint8_t zz[64];
+    __shared__ int4 blk[8];
+    const JpegSyncFrame &F = P.frames[blockIdx.x];
+    const int fs = F.err_block[1];
+    if (fs <= 0) return;  // in step throughout (lane 0 starts at the scan's start: never out of step)
+    stage_tables(F, T);
+    zz[threadIdx.x] = kZigzag[threadIdx.x];
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const JpegSyncState p = F.x[fs - 1];
+    Window win;
+    win.init(F.words, F.nwords - 1, p.pos, F.nbits);
+    const int lim = F.nwords * 32 - 64;
+    int bp = p.pos, u = p.u;
+    int pred[3] = {F.pred[3 * fs], F.pred[3 * fs + 1], F.pred[3 * fs + 2]};
+    int16_t *const co = reinterpret_cast<int16_t *>(blk);
+    for (int b = F.err_block[2]; b < F.nblocks; ++b) {
+        const int m = b / F.bpm, c = F.ucomp[u];
+        const int my = m / F.mcux, mx = m - my * F.mcux;
+        const int by = my * F.cv[c] + F.uby[u], bx = mx * F.ch[c] + F.ubx[u];
+        const JpegHuffTable &dc = T[F.td[c]], &ac = T[4 + F.ta[c]];
+        LongCodes dcl, acl;
+        dcl.load(dc);
+        acl.load(ac);
+#pragma unroll
+        for (int z = 0; z < 8; z++) blk[z] = make_int4(0, 0, 0, 0);
+        int diff = 0;
+        if (!decode_block<true>(win, bp, dc, ac, dcl, acl, diff, co, zz) || bp > lim) {
+            F.err_block[0] = b;  // corrupt (or truncated) from this block on: the zero pass
+            P.error[F.frame] = 1;
+            break;
+        }
+        pred[c] += diff;
+        co[0] = (int16_t)pred[c];
+        int4 *const b4 = reinterpret_cast<int4 *>(F.coef + (F.coef_off[c] + (int64_t)by * F.bw[c] + bx) * 64);
+#pragma unroll
+        for (int z = 0; z < 8; z++) b4[z] = blk[z];
+        u = u + 1 == F.bpm ? 0 : u + 1;
     }
 }
 
@@ -326,8 +388,9 @@ __global__ __launch_bounds__(256) void jpeg_sync_write_kernel(const JpegSyncPara
     }
 }
 
-// Blocks from a frame's err_block on are zero (libjpeg's rule after corrupt data, as the
-// restart-interval kernel does per interval).
+// Blocks from a frame's err_block on are zero: the block holding the bad code and every later one
+// (libjpeg's rule after corrupt data; the restart-interval kernel applies the same rule per
+// interval).
 __global__ __launch_bounds__(256) void jpeg_sync_zero_kernel(const JpegSyncParams P) {
     const JpegSyncFrame &F = P.frames[blockIdx.x];
     const int b0 = F.err_block[0];
@@ -351,6 +414,7 @@ const char *launch_jpeg_sync_scan(const JpegSyncParams &p, int pass, hipStream_t
 const char *launch_jpeg_sync_finish(const JpegSyncParams &p, hipStream_t s) {
     hipLaunchKernelGGL(jpeg_sync_prefix_kernel, dim3(p.nframes), dim3(256), 0, s, p);
     hipLaunchKernelGGL(jpeg_sync_write_kernel, dim3(p.n_wg), dim3(JS_LANES), 0, s, p);
+    hipLaunchKernelGGL(jpeg_sync_serial_kernel, dim3(p.nframes), dim3(64), 0, s, p);
     hipLaunchKernelGGL(jpeg_sync_zero_kernel, dim3(p.nframes), dim3(256), 0, s, p);
     return "jpeg_sync_write_kernel";
 }

@@ -27,7 +27,7 @@ const char *kernel_name(const char *fmt, ...) {
 
 bool form_on(Form f) {
     static const unsigned mask = [] {
-        static const char *const names[FORM_COUNT] = {"dma", "v4", "valu", "valu_db", "rows", "vres", "vstore", "ws", "groups", "dwgap"};
+        static const char *const names[FORM_COUNT] = {"dma", "v4", "valu", "valu_db", "rows", "vres", "vstore", "ws", "groups", "dwgap", "rt"};
         unsigned m = (1u << FORM_COUNT) - 1;
         const char *e = std::getenv("ZARU_HIP_FORMS");
         for (std::string s = e ? e : ""; !s.empty();) {
@@ -85,6 +85,7 @@ const char *launch_elt(const EltParams &p, hipStream_t s) {
 __global__ __launch_bounds__(256) void resize_kernel(const ResizeParams P) {
     const int plane = blockIdx.x;
     const int c = plane / P.N, n = plane - c * P.N;
+    if (P.nact && n >= *P.nact) return;
     const float *src = plane_ptr(P.in, n, c);
     float *dst = P.out + (int64_t)n * P.o_sN + (int64_t)c * P.o_sC;
     const int H = P.in.H, W = P.in.W;

@@ -334,6 +334,47 @@ __global__ __launch_bounds__(64) void hand_manage_kernel(const HandManageParams 
 
 }  // namespace
 
+// one workgroup: a block-wide exclusive scan of the request flags per 1024-stream chunk
+__global__ __launch_bounds__(1024) void due_compact_kernel(const int32_t *pending, int S, const ViewDesc tmpl,
+                                                           int32_t *due, int32_t *ndue, ViewDesc *due_views,
+                                                           uint64_t *total) {
+    __shared__ int wsum[16];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    int base = 0;
+    for (int c0 = 0; c0 < S; c0 += 1024) {
+        const int s = c0 + t;
+        const bool req = s < S && pending[s] != 0;
+        const uint64_t m = __ballot(req);
+        const int in_wave = (int)__popcll(m & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[w] = (int)__popcll(m);
+        __syncthreads();
+        int before = 0, total = 0;
+        for (int i = 0; i < 16; ++i) {
+            before += i < w ? wsum[i] : 0;
+            total += wsum[i];
+        }
+        if (req) {
+            const int k = base + before + in_wave;
+            due[k] = s;
+            ViewDesc v = tmpl;
+            v.frame = (uint32_t)s;
+            due_views[k] = v;
+        }
+        base += total;
+        __syncthreads();  // wsum is rewritten by the next chunk
+    }
+    if (t == 0) {
+        *ndue = base;
+        if (total) *total += (uint64_t)base;
+    }
+}
+
+const char *launch_due_compact(const int32_t *det_pending, int S, const ViewDesc &tmpl, int32_t *due, int32_t *ndue,
+                               ViewDesc *due_views, uint64_t *total, hipStream_t s) {
+    hipLaunchKernelGGL(due_compact_kernel, dim3(1), dim3(1024), 0, s, det_pending, S, tmpl, due, ndue, due_views, total);
+    return "due_compact_kernel";
+}
+
 const char *launch_hand_manage(const HandManageParams &p, hipStream_t s) {
     hipLaunchKernelGGL(hand_manage_kernel, dim3((p.S + 63) / 64), dim3(64), 0, s, p);
     return "hand_manage_kernel";

@@ -21,13 +21,22 @@ struct zr_comm {
 
 namespace {
 
+// A failure of earlier HIP work on this thread (a kernel launch the runtime has not yet checked)
+// must not vanish inside a communicator call: every entry point first takes the thread's pending
+// HIP error and, if there is one, returns it as ZR_ERR_DEVICE without calling RCCL.
+int pending_hip_error(const char *where) {
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess) return ZR_OK;
+    return zr_internal::set_error(ZR_ERR_DEVICE, std::string(where) + ": pending HIP error from earlier work: " +
+                                                     hipGetErrorString(e));
+}
+
 // RCCL's own HIP calls (capture queries on the caller's stream among them) may leave the thread's
 // last-error slot set although the call succeeded; the runtime's next hipGetLastError() check after
-// a kernel launch would then report RCCL's stale status as its own failure.  Every entry point
-// here clears it before returning.
-struct ClearLastError {
-    ~ClearLastError() { (void)hipGetLastError(); }
-};
+// a kernel launch would then report RCCL's stale status as its own failure.  So after an RCCL call
+// (and only then: anything pending before it was already taken by pending_hip_error) the slot is
+// cleared.
+void clear_rccl_status() { (void)hipGetLastError(); }
 
 int nccl_err(const char *what, ncclResult_t r) {
     return zr_internal::set_error(ZR_ERR_DEVICE, std::string(what) + ": " + ncclGetErrorString(r));
@@ -49,32 +58,38 @@ int guarded(F &&body) noexcept {
 extern "C" {
 
 int zr_comm_unique_id(uint8_t id[128]) {
-    ClearLastError clear;
     return guarded([&]() -> int {
         static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
         if (!id) return zr_internal::set_error(ZR_ERR_INVALID_ARGUMENT, "null id");
+        if (int e = pending_hip_error("zr_comm_unique_id")) return e;
         ncclUniqueId u;
-        if (ncclResult_t r = ncclGetUniqueId(&u)) return nccl_err("ncclGetUniqueId", r);
+        const ncclResult_t r = ncclGetUniqueId(&u);
+        clear_rccl_status();
+        if (r) return nccl_err("ncclGetUniqueId", r);
         std::memcpy(id, &u, sizeof u);
         return ZR_OK;
     });
 }
 
 int zr_comm_create(const uint8_t id[128], int nranks, int rank, int device, zr_comm **out) {
-    ClearLastError clear;
     return guarded([&]() -> int {
         if (!id || !out || nranks <= 0 || rank < 0 || rank >= nranks)
             return zr_internal::set_error(ZR_ERR_INVALID_ARGUMENT, "bad communicator arguments");
         *out = nullptr;
-        if (hipSetDevice(device) != hipSuccess)
+        if (int e = pending_hip_error("zr_comm_create")) return e;
+        if (hipSetDevice(device) != hipSuccess) {
+            (void)hipGetLastError();
             return zr_internal::set_error(ZR_ERR_DEVICE, "no HIP device " + std::to_string(device));
+        }
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof u);
         auto *c = new zr_comm;
         c->nranks = nranks;
         c->rank = rank;
         c->device = device;
-        if (ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank)) {
+        const ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+        clear_rccl_status();
+        if (r) {
             delete c;
             return nccl_err("ncclCommInitRank", r);
         }
@@ -84,21 +99,32 @@ int zr_comm_create(const uint8_t id[128], int nranks, int rank, int device, zr_c
 }
 
 void zr_comm_destroy(zr_comm *c) {
-    ClearLastError clear;
     if (!c) return;
-    if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->comm) {
+        // teardown: RCCL's status is cleared; an error of earlier work is reported by the caller's
+        // own synchronisation, which sees the failed stream, not by this slot
+        (void)ncclCommDestroy(c->comm);
+        clear_rccl_status();
+    }
     delete c;
 }
 
+int zr_comm_size(const zr_comm *c, int *nranks) {
+    if (!c || !nranks) return zr_internal::set_error(ZR_ERR_INVALID_ARGUMENT, "null communicator or output");
+    *nranks = c->nranks;
+    return ZR_OK;
+}
+
 int zr_comm_all_gather_async(zr_comm *c, const void *d_send, void *d_recv, size_t bytes, void *hip_stream) {
-    ClearLastError clear;
     return guarded([&]() -> int {
         if (!c || !c->comm || !d_send || !d_recv)
             return zr_internal::set_error(ZR_ERR_INVALID_ARGUMENT, "null communicator or buffer");
+        if (int e = pending_hip_error("zr_comm_all_gather_async")) return e;
         if (bytes == 0) return ZR_OK;
         // bytes as ncclChar elements: the records are opaque 32-bit words (f32 and u32 bits)
-        if (ncclResult_t r = ncclAllGather(d_send, d_recv, bytes, ncclChar, c->comm, (hipStream_t)hip_stream))
-            return nccl_err("ncclAllGather", r);
+        const ncclResult_t r = ncclAllGather(d_send, d_recv, bytes, ncclChar, c->comm, (hipStream_t)hip_stream);
+        clear_rccl_status();
+        if (r) return nccl_err("ncclAllGather", r);
         return ZR_OK;
     });
 }

@@ -1175,6 +1175,7 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook
         g.o_sN = out.sN;
         g.o_sC = out.sC;
         g.o_sP = out.sP;
+        g.nact = b.nact;
         return g;
     };
     auto dwpw_of = [&](const Step &s) {
@@ -1215,6 +1216,7 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook
         d.dw_w = W + s.dw_w_off;
         d.dw_b = W + s.dw_b_off;
         d.dw_act = act_of(s.dw_act, W);
+        g.nact = b.nact;
         return d;
     };
     for (size_t si = 0; si < plan.steps.size(); ++si) {
@@ -1295,6 +1297,7 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook
                 sp.w = W + s.w_off;
                 sp.bias = W + s.b_off;
                 sp.act = act_of(s.pre, W);
+                sp.nact = b.nact;
                 kname = launch_stem(sp, pre, stream);
                 if (hook) hook->after(stream, kname, (pre ? s.bytes_pre : s.bytes) * b.N, s.flops * b.N);
                 continue;
@@ -1346,6 +1349,7 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook
             r.OW = s.out.W;
             r.scale_y = s.scale_y;
             r.scale_x = s.scale_x;
+            r.nact = b.nact;
             kname = launch_resize(r, stream);
             break;
         }

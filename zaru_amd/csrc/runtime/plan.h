@@ -100,6 +100,8 @@ struct Binding {
     const float *weights = nullptr;
     // when set, the input comes from RGBA frames through these views (plan.input_fusable)
     const PreprocParams *pre = nullptr;
+    // device image count (may be null): images >= *nact need not be computed (GemmParams::nact)
+    const int *nact = nullptr;
 };
 
 // Optional per-launch hook (profiling): called before and after every kernel launch with the

@@ -237,7 +237,8 @@ struct CtxLock {
 
 // enqueue the plan on `stream` with a context's workspace
 int enqueue(zr_session *s, Ctx *c, int N, const float *input, int64_t in_sN, int64_t in_sC,
-            float *const *outs, hipStream_t stream, const zr::PreprocParams *pre = nullptr) {
+            float *const *outs, hipStream_t stream, const zr::PreprocParams *pre = nullptr,
+            const int *d_nact = nullptr) {
     const int Ns = (N + 3) / 4 * 4;  // zr::Binding::Ns
     const size_t need = (size_t)s->plan.arena_per_image * (size_t)Ns;
     // kernels address every tensor with 32-bit element offsets (kernels/epilogue.h)
@@ -257,6 +258,7 @@ int enqueue(zr_session *s, Ctx *c, int N, const float *input, int64_t in_sN, int
     b.arena = c->arena;
     b.weights = s->weights;
     b.pre = pre;
+    b.nact = d_nact;
     {
         const bool prof = s->prof.on.load();  // one read: the hook and its lock agree
         std::unique_lock<std::mutex> pl(s->prof.mu, std::defer_lock);
@@ -542,7 +544,7 @@ int zr_session_run(zr_session *s, size_t batch, const float *const *inputs, size
 
 static int views_common(zr_session *s, Ctx *c, const zr_frame *frames, size_t nf, const zr_view *views,
                         const uint32_t *view_frame, size_t nv, float lo, float hi, float *const *outs,
-                        hipStream_t stream, const zr::ViewDesc *d_views = nullptr) {
+                        hipStream_t stream, const zr::ViewDesc *d_views = nullptr, const int *d_nact = nullptr) {
     const int64_t hw = (int64_t)s->plan.in_H * s->plan.in_W;
     if (s->plan.in_C != 3) return set_err(ZR_ERR_SHAPE, "view sampling needs a 3-channel input");
     if (!(hi > lo)) return set_err(ZR_ERR_INVALID_ARGUMENT, "ColorMapper range must satisfy end > start");
@@ -559,7 +561,7 @@ static int views_common(zr_session *s, Ctx *c, const zr_frame *frames, size_t nf
     p.lo = lo;
     p.adjust = (hi - lo) / 255.0f;  // nn/mod.rs:162
     if (s->plan.input_fusable)  // the stem samples the frames itself: no input tensor at all
-        return enqueue(s, c, (int)nv, nullptr, 0, 0, outs, stream, &p);
+        return enqueue(s, c, (int)nv, nullptr, 0, 0, outs, stream, &p, d_nact);
     if (int rc = grow(c->input, c->input_floats, (size_t)hw * 3 * nv)) return rc;
     p.out = c->input;
     p.o_sN = hw;                    // CNHW straight into the plan's input layout
@@ -574,7 +576,7 @@ static int views_common(zr_session *s, Ctx *c, const zr_frame *frames, size_t nf
         if (prof) s->prof.after(stream, k, 16.0 * (double)hw * nv, 0.0);
     }
     HIP_TRY(hipGetLastError());
-    return enqueue(s, c, (int)nv, c->input, hw, hw * (int64_t)nv, outs, stream);
+    return enqueue(s, c, (int)nv, c->input, hw, hw * (int64_t)nv, outs, stream, nullptr, d_nact);
 }
 
 int zr_cnn_estimate_views_async(zr_session *s, const zr_frame *frames, size_t n_frames,
@@ -660,10 +662,11 @@ int zr_track_update_async(zr_track_state *d_state, size_t n, const zr_track_cfg 
     });
 }
 
-int zr_detect_post_async(const float *d_logits, const float *d_boxes, const float *d_anchors,
-                         const float *d_letterbox, size_t n, const zr_detpost_cfg *cfg, int32_t *d_count,
-                         float *d_dets, size_t dcap, float *d_records, size_t rmax, uint32_t first_id,
-                         uint32_t id_stride, void *hip_stream) {
+static int detect_post_impl(const float *d_logits, const float *d_boxes, const float *d_anchors,
+                            const float *d_letterbox, size_t n, const zr_detpost_cfg *cfg, int32_t *d_count,
+                            float *d_dets, size_t dcap, float *d_records, size_t rmax, uint32_t first_id,
+                            uint32_t id_stride, int32_t *d_ties, const int32_t *d_map, const int32_t *d_nact,
+                            void *hip_stream) {
     return guarded([&]() -> int {
         if (!d_logits || !d_boxes || !d_anchors || !d_letterbox || !cfg || !d_count || (!d_dets && dcap))
             return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument");
@@ -694,11 +697,31 @@ int zr_detect_post_async(const float *d_logits, const float *d_boxes, const floa
         p.rmax = (int)rmax;
         p.first_id = first_id;
         p.id_stride = id_stride;
+        p.ties = d_ties;
+        p.map = d_map;
+        p.nact = d_nact;
         if (zr::det_post_lds(p.A) > 128 * 1024) return set_err(ZR_ERR_INVALID_ARGUMENT, "too many anchors");
         zr::launch_det_post(p, (hipStream_t)hip_stream);
         HIP_TRY(hipGetLastError());
         return ZR_OK;
     });
+}
+
+int zr_detect_post_async(const float *d_logits, const float *d_boxes, const float *d_anchors,
+                         const float *d_letterbox, size_t n, const zr_detpost_cfg *cfg, int32_t *d_count,
+                         float *d_dets, size_t dcap, float *d_records, size_t rmax, uint32_t first_id,
+                         uint32_t id_stride, int32_t *d_ties, void *hip_stream) {
+    return detect_post_impl(d_logits, d_boxes, d_anchors, d_letterbox, n, cfg, d_count, d_dets, dcap, d_records, rmax,
+                            first_id, id_stride, d_ties, nullptr, nullptr, hip_stream);
+}
+
+int zr_detect_post_mapped_async(const float *d_logits, const float *d_boxes, const float *d_anchors,
+                                const float *d_letterbox, size_t n, const int32_t *d_map, const int32_t *d_nframes,
+                                const zr_detpost_cfg *cfg, int32_t *d_count, float *d_dets, size_t dcap,
+                                int32_t *d_ties, void *hip_stream) {
+    if (!d_map || !d_nframes) return set_err(ZR_ERR_INVALID_ARGUMENT, "null frame map or count");
+    return detect_post_impl(d_logits, d_boxes, d_anchors, d_letterbox, n, cfg, d_count, d_dets, dcap, nullptr, 0, 0, 1,
+                            d_ties, d_map, d_nframes, hip_stream);
 }
 
 int zr_track_seed_detections_async(const int32_t *d_count, const float *d_dets, size_t dcap, const float *d_forced,
@@ -814,6 +837,35 @@ int zr_cnn_estimate_device_views_async(zr_session *s, const zr_frame *frames, si
         HIP_TRY(hipSetDevice(s->device));
         return views_common(s, c, frames, n_frames, nullptr, nullptr, n_views, lo, hi, d_outputs,
                             (hipStream_t)hip_stream, reinterpret_cast<const zr::ViewDesc *>(d_views));
+    });
+}
+
+int zr_cnn_estimate_device_views_count_async(zr_session *s, const zr_frame *frames, size_t n_frames,
+                                             const zr_view_desc *d_views, size_t n_views, const int32_t *d_count,
+                                             float lo, float hi, float *const *d_outputs, void *hip_stream) {
+    return guarded([&]() -> int {
+        if (int rc = check_session(s)) return rc;
+        if (!frames || !d_views || !d_outputs || !d_count || n_views == 0 || n_frames == 0)
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument or no views");
+        Ctx *c = s->acquire();
+        if (!c) return set_err(ZR_ERR_DEVICE, "cannot create execution context");
+        CtxLock lk(c);
+        HIP_TRY(hipSetDevice(s->device));
+        return views_common(s, c, frames, n_frames, nullptr, nullptr, n_views, lo, hi, d_outputs,
+                            (hipStream_t)hip_stream, reinterpret_cast<const zr::ViewDesc *>(d_views), d_count);
+    });
+}
+
+int zr_due_compact_async(const int32_t *d_det_pending, size_t n, const zr_view_desc *view_template, int32_t *d_due,
+                         int32_t *d_ndue, zr_view_desc *d_due_views, uint64_t *d_total, void *hip_stream) {
+    return guarded([&]() -> int {
+        if (!d_det_pending || !view_template || !d_due || !d_ndue || !d_due_views)
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument");
+        if (n == 0 || n > (1u << 24)) return set_err(ZR_ERR_INVALID_ARGUMENT, "bad stream count");
+        zr::launch_due_compact(d_det_pending, (int)n, *reinterpret_cast<const zr::ViewDesc *>(view_template), d_due,
+                               d_ndue, reinterpret_cast<zr::ViewDesc *>(d_due_views), d_total, (hipStream_t)hip_stream);
+        HIP_TRY(hipGetLastError());
+        return ZR_OK;
     });
 }
 

@@ -105,7 +105,9 @@ struct JpegSyncFrame {
     int2 *start;                  // [nseg] the (pos, u) the lane's checkpoints were decoded from
     int32_t *base;                // [nseg] first block index (-1: nothing to write)
     int32_t *pred;                // [nseg][3] DC predictors at the lane's start
-    int32_t *err_block;           // [1] blocks from here on are zero (nblocks: none)
+    int32_t *err_block;           // [4]: [0] blocks from here on are zero (nblocks: none);
+                                  // [1] first lane out of step after the sync passes (-1: none),
+                                  // [2] its first block: the serial kernel decodes from there
     int frame;                    // index into the call's error flags
 };
 struct JpegSyncParams {
@@ -118,7 +120,8 @@ struct JpegSyncParams {
 constexpr int JS_PASSES = 32;     // sync passes launched per call at most (each returns at once
                                   // once a pass changed nothing)
 constexpr int JS_MAX_BITS_PER_BLOCK = 600;  // denser scans decode on the host
-// pass 0: the guessed decode, 1..JS_PASSES: sync passes; then prefix, write and zero fill
+// pass 0: the guessed decode, 1..passes (<= JS_PASSES): sync passes; then prefix, write, the serial
+// decode of a frame whose sync passes ran out, and the zero fill
 const char *launch_jpeg_sync_scan(const JpegSyncParams &p, int pass, hipStream_t s);
 const char *launch_jpeg_sync_finish(const JpegSyncParams &p, hipStream_t s);
 

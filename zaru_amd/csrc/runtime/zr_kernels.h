@@ -57,6 +57,10 @@ struct GemmParams {
     // output (m, j) at out + n*o_sN + m*o_sC + q*o_sP
     float *out;
     int64_t o_sN, o_sC, o_sP;
+    // device image count (may be null): workgroups whose columns all lie in images >= *nact may
+    // skip their work -- those images' outputs are then undefined (the BlazePalm launches of the
+    // device HandTracker run over the streams due for detection only, hand/tracking.rs:210-218)
+    const int *nact;
 };
 
 // ---------------------------------------------------------------- depthwise conv
@@ -99,6 +103,7 @@ struct ResizeParams {    // bilinear, half_pixel, edge clamp
     int64_t o_sN, o_sC;
     int N, OH, OW;
     float scale_y, scale_x;  // in/out ratio
+    const int *nact;         // as GemmParams::nact
 };
 
 struct GapParams {
@@ -163,6 +168,7 @@ struct StemParams {
     const float *w;      // [3][k][k][32] (output channel innermost, zero-padded to 32)
     const float *bias;   // [>= 32]
     Act act;
+    const int *nact;     // as GemmParams::nact
 };
 
 // Depthwise KxK conv feeding a 1x1 conv (BlazeBlock / inverted-residual tail) in one launch.
@@ -190,7 +196,8 @@ struct DwPwParams {
 //   ws: warp-specialized persistent MFMA dwpw (dwpw_ws.hip)
 //   groups: sibling steps launched as one grid (plan.cpp group_siblings, kernels/group.h)
 //   dwgap: depthwise + global average pool in one launch (plan.cpp fuse_dw_gap)
-enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_VRES, FORM_VSTORE, FORM_WS, FORM_GROUPS, FORM_DWGAP, FORM_COUNT };
+//   rt: row-task depthwise inside the LDS-DMA MFMA dwpw (dwpw_dma_body, RT > 0)
+enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_VRES, FORM_VSTORE, FORM_WS, FORM_GROUPS, FORM_DWGAP, FORM_RT, FORM_COUNT };
 bool form_on(Form f);
 
 bool stem_supported(int cin, int k, int stride, int cout);

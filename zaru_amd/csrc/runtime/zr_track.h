@@ -58,6 +58,10 @@ struct DetPostParams {
     float *rec;             // [N][2 + 20 rmax] all-gather records (may be null)
     int rmax;
     uint32_t first_id, id_stride;
+    int *ties;              // [N][2] {candidates, candidates sharing their confidence} (may be null)
+    // (both may be null) frame f < *nact writes slot map[f] of count / dets / rec / ties and uses
+    // letterbox[map[f]]; frames >= *nact do nothing (the device HandTracker's due streams)
+    const int *map, *nact;
 };
 const char *launch_det_post(const DetPostParams &p, hipStream_t s);
 size_t det_post_lds(int anchors);
@@ -107,6 +111,10 @@ struct HandManageParams {
     int asp_w, asp_h;
 };
 const char *launch_hand_manage(const HandManageParams &p, hipStream_t s);
+// The streams whose detection hand_manage requested (det_pending[s] != 0), in stream order: due[k]
+// = s for k < *ndue, and due_views[k] = the template view with frame = s (one workgroup).
+const char *launch_due_compact(const int32_t *det_pending, int S, const ViewDesc &tmpl, int32_t *due, int32_t *ndue,
+                               ViewDesc *due_views, uint64_t *total, hipStream_t s);
 
 // fn: 0 sinf, 1 cosf, 2 expf, 3 atanf, 4 atan2f(a, b) -- glibc_math.h on the device
 const char *launch_glibc_math(int fn, const float *a, const float *b, float *out, int64_t n, hipStream_t s);

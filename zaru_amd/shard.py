@@ -5,7 +5,11 @@ independent: nothing crosses frames except tracker ROIs (crates/zaru/src/landmar
 hand/tracking.rs:22). So the path shards by frame. Each rank (one process per GPU) runs the
 whole detect→track pipeline on its own frames. Frame i goes to rank i mod G, which is weak
 scaling: per-rank work stays fixed as G grows. The only exchange is one all-gather per step of
-fixed-size detection records (RCCL over xGMI with the "nccl" backend; gloo in the CPU tests).
+fixed-size detection records. On GPUs it runs natively: the post-processing kernel writes the
+records on the device and the pipeline all-gathers them over RCCL itself
+(``DetectTrackPipeline.enable_records`` → ``zr_comm_all_gather_async``); nothing in this module
+is on that path. What lives here is the host side of the same exchange over a gloo group: the
+record layout, the frame → rank map, and the gather the CPU tests and the shared-GPU dry run use.
 Landmarks stay rank-local.
 
 Record layout (``zaru_amd.host.pack_detection_records``, width 2 + 20·rmax f32):
@@ -46,45 +50,38 @@ def unpack_records(recs: np.ndarray, rmax: int = REC_DETS) -> Dict[int, List[Tup
 
 
 def all_gather_records(local, group=None):
-    """All-gather one [B, W] f32 tensor of records from every rank into [world·B, W] (rank-major).
-    Uses all_gather_into_tensor on RCCL; gloo lacks it, so there it gathers a list."""
+    """All-gather one [B, W] f32 CPU tensor of records from every rank of a gloo group into
+    [world·B, W] (rank-major)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    out = torch.empty((world * local.shape[0], local.shape[1]), dtype=local.dtype, device=local.device)
-    if dist.get_backend(group) == "nccl":
-        dist.all_gather_into_tensor(out, local.contiguous(), group=group)
-    else:
-        dist.all_gather(list(out.chunk(world)), local.contiguous(), group=group)
+    out = torch.empty((world * local.shape[0], local.shape[1]), dtype=local.dtype)
+    dist.all_gather(list(out.chunk(world)), local.contiguous(), group=group)
     return out
 
 
 class RecordGather:
-    """The per-step all-gather of detection records, overlapped with the next steps.
+    """The per-step all-gather of host records over a gloo group, overlapped with the next steps
+    (the shared-GPU dry run of bench.py and the CPU tests; GPU ranks gather on the device).
 
-    ``submit(recs)`` takes one step's host records ([B, W] f32, ``DetectTrackPipeline.
-    detection_records``), stages them in a pinned buffer, copies them to the device and starts
-    the all-gather asynchronously (``async_op=True``: RCCL runs it on its own stream, gloo on its
-    own thread), then returns at once, so the pipeline's next step starts while the collective is
-    in flight.  Two slots alternate; a slot is reused only after its previous copy and gather
-    completed.  ``finish()`` waits for the collectives still in flight; ``result(step)`` is the
-    [world * B, W] gathered tensor of a finished step (rank-major, frames of rank r first).
-    One collective per step and no other: SURVEY.md §8e.
+    ``submit(recs)`` takes one step's records ([B, W] f32), copies them into a slot and starts the
+    all-gather asynchronously (``async_op=True``: gloo runs it on its own thread), then returns at
+    once, so the pipeline's next step starts while the collective is in flight.  Two slots
+    alternate; a slot is reused only after its previous gather completed.  ``finish()`` waits for
+    the collectives still in flight; ``result(step)`` is the [world * B, W] gathered tensor of a
+    finished step (rank-major, frames of rank r first).  One collective per step and no other:
+    SURVEY.md §8e.
     """
 
-    def __init__(self, rows: int, width: int, device, group=None):
+    def __init__(self, rows: int, width: int, group=None):
         import torch
         import torch.distributed as dist
+        if dist.get_backend(group) != "gloo":
+            raise ValueError("RecordGather is the gloo (host) gather; GPU ranks use enable_records")
         self.group = group
         self.world = dist.get_world_size(group)
-        self.nccl = dist.get_backend(group) == "nccl"
-        self.device = torch.device(device)
-        cuda = self.device.type == "cuda"
-        self.host = [torch.empty((rows, width), dtype=torch.float32, pin_memory=cuda) for _ in range(2)]
-        self.inp = [torch.empty((rows, width), dtype=torch.float32, device=self.device) for _ in range(2)]
-        self.out = [torch.empty((self.world * rows, width), dtype=torch.float32, device=self.device)
-                    for _ in range(2)]
-        self.copied = [torch.cuda.Event() if cuda else None for _ in range(2)]
+        self.inp = [torch.empty((rows, width), dtype=torch.float32) for _ in range(2)]
+        self.out = [torch.empty((self.world * rows, width), dtype=torch.float32) for _ in range(2)]
         self.work = [None, None]
         self.step_of = [-1, -1]
         self.steps = 0
@@ -93,35 +90,20 @@ class RecordGather:
         if self.work[k] is not None:
             self.work[k].wait()
             self.work[k] = None
-        if self.copied[k] is not None:
-            self.copied[k].synchronize()  # the pinned slot may be rewritten
 
     def submit(self, recs: np.ndarray) -> None:
-        import torch
         import torch.distributed as dist
         k = self.steps & 1
         self._wait(k)
-        self.host[k].numpy()[...] = recs
-        if self.device.type == "cuda":
-            self.inp[k].copy_(self.host[k], non_blocking=True)
-            self.copied[k].record()
-        else:
-            self.inp[k].copy_(self.host[k])
-        if self.nccl:
-            self.work[k] = dist.all_gather_into_tensor(self.out[k], self.inp[k], group=self.group,
-                                                       async_op=True)
-        else:
-            self.work[k] = dist.all_gather(list(self.out[k].chunk(self.world)), self.inp[k],
-                                           group=self.group, async_op=True)
+        self.inp[k].numpy()[...] = recs
+        self.work[k] = dist.all_gather(list(self.out[k].chunk(self.world)), self.inp[k],
+                                       group=self.group, async_op=True)
         self.step_of[k] = self.steps
         self.steps += 1
 
     def finish(self) -> None:
         for k in range(2):
             self._wait(k)
-        if self.device.type == "cuda":
-            import torch
-            torch.cuda.current_stream(self.device).synchronize()
 
     def result(self, step: int):
         for k in range(2):
