@@ -325,6 +325,7 @@ def cpu_baseline(kind, seconds, batch, seed, P=None):
             "rois_per_s": round(sum(r["rois"] / r["seconds"] for r in res), 2),
             "frames_per_s": round(sum(r["frames"] / r["seconds"] for r in res), 2),
             "cpu": cpu_model(), "stage_ms_per_frame": stage,
+            "stage_clock": "process CPU time per frame (the processes share the cgroup's cores)",
             "label": "reference-semantics C restatement (ORT/tract unavailable): oracle/ direct f32 "
                      "convolutions, glibc-exact geometry, 1 thread per process",
             "sample": f"{frames} synthetic 1080p frames ({sum(r['rois'] for r in res)} ROIs) of the "
@@ -876,7 +877,14 @@ def hand_line(H, args, device, traffic=None):
     t = run_steps([w], args.hand_steps, None, 0, 1, None)[0]
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    rpf = t["rois"] / max(1, t["frames"])
+    bpf = (SURVEY_BYTES[w.det] + 16.0 * 192 * 192 + rpf * (SURVEY_BYTES[w.lm] + 16.0 * 224 * 224))
+    gbs = t["frames"] / elapsed * bpf / 1e9
     out = {"value": round(t["rois"] / elapsed, 1), "unit": "hand ROIs/s",
+           "pipeline_roofline": {"model": "SURVEY.md §8d bytes per frame: palm + 192^2 preprocessing + "
+                                          "hand landmark + 224^2 preprocessing per ROI",
+                                 "bytes_per_frame": round(bpf), "achieved_GBs_per_gpu": round(gbs, 1),
+                                 "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4)},
            "frames_per_s": round(t["frames"] / elapsed, 1),
            "tracked_per_s": round(t["tracked"] / elapsed, 1),
            "ms_per_step": round(1e3 * elapsed / args.hand_steps, 3), "steps": args.hand_steps,

@@ -62,43 +62,46 @@ def main():
     stage = {"preproc_ms": 0.0, "det_infer_ms": 0.0, "extract_nms_ms": 0.0,
              "lm_infer_ms": 0.0, "lm_map_ms": 0.0}
     clk = time.perf_counter
+    # per-stage figures in process CPU time: with more processes than the cgroup's cores, wall
+    # spans of a stage would include the time the process waited for a core
+    sclk = time.process_time
     nframes = nrois = ntracked = 0
     t_start = clk()
     f = args.worker
     while clk() - t_start < args.seconds:
         img = fs.frame(f % args.batch)
         h, w = img.shape[:2]
-        t = clk()
+        t = sclk()
         r = O.grow_to_fit_aspect(O.Rect.from_top_left(0, 0, w, h), din, din)
         v = O.view_compose(O.view_full(w, h), r)
         x = O.preproc(img, v, din, din, lo, 1.0)
-        t1 = clk()
+        t1 = sclk()
         reg, cls = det.run(x[None])
-        t2 = clk()
+        t2 = sclk()
         dets = O.detect_post(kind, reg[0], cls[0], w, h, din, din)
         if dets:
             rois = [O.RRect(O.grow_rel(d.rect, grow) if grow else d.rect, 0.0 if face else d.angle)
                     for d in dets[:1 if face else 4]]  # max_rois_per_frame of the GPU pipeline
         else:
             rois = [O.RRect(O.Rect(*fr[:4]), fr[4]) for fr in forced[f % args.batch]]
-        t3 = clk()
+        t3 = sclk()
         stage["preproc_ms"] += (t1 - t) * 1e3
         stage["det_infer_ms"] += (t2 - t1) * 1e3
         stage["extract_nms_ms"] += (t3 - t2) * 1e3
         for roi in rois:
-            t = clk()
+            t = sclk()
             vr = O.RRect(O.grow_to_fit_aspect(roi.rect, 1, 1), roi.rad)
             view = O.view_compose(O.view_full(w, h), vr)
             lrect = O.grow_to_fit_aspect(O.Rect.from_top_left(0, 0, view.rect.w, view.rect.h), 1, 1)
             xl = O.preproc(img, O.view_compose(view, lrect), lin, lin, lo, 1.0)
-            t1 = clk()
+            t1 = sclk()
             outs = lm.run(xl[None])
-            t2 = clk()
+            t2 = sclk()
             pos = O.estimator_map(outs[0].reshape(-1, 3), lrect, lin)  # Estimator maps first
             if O.landmark_confidence(lkind, outs) >= 0.5:  # then the tracker's loss check
                 O.tracker_update(pos, vr, roi.rad, O.landmark_angle(lkind, pos), pad)
                 ntracked += 1
-            t3 = clk()
+            t3 = sclk()
             stage["preproc_ms"] += (t1 - t) * 1e3
             stage["lm_infer_ms"] += (t2 - t1) * 1e3
             stage["lm_map_ms"] += (t3 - t2) * 1e3

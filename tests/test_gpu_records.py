@@ -101,12 +101,12 @@ def test_records_world_must_match_the_communicator(frames):
 
 
 def test_comm_reports_a_pending_hip_error():
-    import ctypes
     from zaru_amd._lib import Comm, DeviceBuffer, ZaruError
     comm = Comm(Comm.unique_id(), 1, 0, 0)
     src, dst = DeviceBuffer(256), DeviceBuffer(256)
-    hip = ctypes.CDLL("libamdhip64.so")
-    assert hip.hipSetDevice(ctypes.c_int(4096)) != 0  # a failed HIP call: its error is now pending
+    # a HIP call of the library's own runtime that fails (pitch < width): its error is now pending
+    from zaru_amd._lib import lib
+    assert lib().zr_memcpy2d_async(dst.ptr, 4, src.ptr, 256, 256, 1, 2, None) == -3
     with pytest.raises(ZaruError, match="pending HIP error") as e:
         comm.all_gather_async(src.ptr, dst.ptr, 256)
     assert e.value.code == -3
