@@ -45,7 +45,8 @@ SWITCHES = {
     "no_groups": "-groups",
     "no_dwgap": "-dwgap",
     "no_rt": "-rt",
-    "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws,-groups,-dwgap,-rt",
+    "no_ir": "-ir",
+    "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws,-groups,-dwgap,-rt,-ir",
 }
 
 

@@ -1,6 +1,8 @@
 """Side-by-side per-launch times (us) of the last repetition in two rocprofv3 kernel traces of
 tools/kernel_probe.py (e.g. a form switched on / off).  Usage: python tools/layer_cmp.py A.csv B.csv"""
-import csv,sys
+import csv,sys,os
+sys.path.insert(0,os.path.dirname(os.path.abspath(__file__)))
+from pmc_table import sym
 def load(path,reps=5):
     rows=[r for r in csv.DictReader(open(path)) if "zr::" in r["Kernel_Name"]]
     rows.sort(key=lambda r:int(r["Start_Timestamp"]))
@@ -8,7 +10,7 @@ def load(path,reps=5):
     out=[]
     for r in rows[-n:]:
         us=(int(r["End_Timestamp"])-int(r["Start_Timestamp"]))/1000
-        k=r["Kernel_Name"]; k=k[k.find("zr::")+4:].split("(")[0].replace(" ","")
+        k=sym(r["Kernel_Name"])
         out.append((k,us))
     return out
 a=load(sys.argv[1]); b=load(sys.argv[2])

@@ -14,8 +14,23 @@ CLK_GHZ, SIMDS = 2.4, 1024
 
 
 def sym(name):
-    name = name.replace("(anonymous namespace)::", "").split("(")[0]
-    return (name.split("zr::", 1)[-1] if "zr::" in name else name.split(" ")[-1]).replace(" ", "")
+    """Kernel symbol without return type, namespaces and parameter list.  The parameter list is
+    the first '(' outside the template arguments (those may hold casts such as '(zr::X)1')."""
+    name = name.replace("(anonymous namespace)::", "")
+    depth = 0
+    for i, ch in enumerate(name):
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            name = name[:i]
+            break
+    name = name.strip()
+    if name.startswith("void "):
+        name = name[5:]
+    name = name.replace("zr::", "").replace(" ", "")
+    return name or "?"
 
 
 def main():

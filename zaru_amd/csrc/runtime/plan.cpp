@@ -84,6 +84,7 @@ class Compiler {
     void finalize_outputs();
     void fuse_dw_gap();
     void group_siblings();
+    void mark_inverted_residuals();
     void allocate();
 };
 
@@ -899,6 +900,22 @@ void Compiler::fuse_dw_gap() {
     }
 }
 
+// Expand 1x1 -> (depthwise -> 1x1) pairs whose expanded tensor nothing else reads: the executor
+// may launch them as one inverted-residual kernel (ir.hip), the expanded tensor never stored.
+void Compiler::mark_inverted_residuals() {
+    std::vector<int> reads(P.storage_size.size(), 0);
+    for (const Step &s : P.steps)
+        for (const TRef *r : {&s.in, &s.in2})
+            if (r->kind == 0 && r->id >= 0) reads[r->id]++;
+    for (size_t i = 0; i + 1 < P.steps.size(); i++) {
+        Step &e = P.steps[i];
+        const Step &d = P.steps[i + 1];
+        e.ir = e.kind == S_GEMM && e.group == 1 && d.group == 1 && e.KK == 1 && e.res_mode == 0 && e.out.kind == 0 &&
+               e.out.c_off == 0 && e.in.kind == 0 && e.in.c_off == 0 && d.kind == S_DWPW && d.in.kind == 0 &&
+               d.in.id == e.out.id && d.in.c_off == 0 && reads[e.out.id] == 1 && e.M == d.K;
+    }
+}
+
 void Compiler::group_siblings() {
     const int n = (int)P.steps.size();
     if (n < 2) return;
@@ -969,14 +986,24 @@ void Compiler::allocate() {
     const size_t ns = P.storage_size.size();
     std::vector<int> first(ns, 1 << 30), last(ns, -1);
     int time = -1;
+    std::vector<int> tof(P.steps.size());
     for (size_t i = 0; i < P.steps.size(); i++) {
         const Step &s = P.steps[i];
         if (s.group != 0) ++time;
+        tof[i] = time;
         for (const TRef *r : {&s.in, &s.in2, &s.out})
             if (r->kind == 0 && r->id >= 0) {
                 first[r->id] = std::min(first[r->id], time);
                 last[r->id] = std::max(last[r->id], time);
             }
+    }
+    // a fused inverted residual (Step::ir) reads the expand's input and writes the projection's
+    // output in ONE launch: the two must not share memory, so each is live across both steps
+    for (size_t i = 0; i + 1 < P.steps.size(); i++) {
+        if (!P.steps[i].ir) continue;
+        const TRef &x = P.steps[i].in, &o = P.steps[i + 1].out;
+        if (x.kind == 0 && x.id >= 0) last[x.id] = std::max(last[x.id], tof[i + 1]);
+        if (o.kind == 0 && o.id >= 0) first[o.id] = std::min(first[o.id], tof[i]);
     }
     std::vector<int> order(ns);
     for (size_t i = 0; i < ns; i++) order[i] = (int)i;
@@ -1072,6 +1099,7 @@ bool Compiler::run(const std::vector<uint32_t> &sel) {
     P.input_fusable = readers == 1 && P.steps[reader].kind == S_DIRECT && P.steps[reader].stem;
     if (form_on(FORM_DWGAP)) fuse_dw_gap();
     if (form_on(FORM_GROUPS)) group_siblings();
+    if (form_on(FORM_IR)) mark_inverted_residuals();
     allocate();
     return true;
 }
@@ -1221,6 +1249,22 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook
     };
     for (size_t si = 0; si < plan.steps.size(); ++si) {
         const Step &s = plan.steps[si];
+        if (s.ir && si + 1 < plan.steps.size()) {
+            // expand + depthwise + projection in one launch (mark_inverted_residuals); nullptr: the
+            // shapes do not fit the fused kernel, so both run on their own below
+            const Step &s2 = plan.steps[si + 1];
+            const GemmParams ge = gemm_of(s);
+            const DwPwParams dp = dwpw_of(s2);
+            if (hook) hook->before(stream);
+            if (const char *kname = launch_ir(ge, dp, stream)) {
+                // fused-boundary bytes: the block input (+ residual) and the output
+                const double bytes = s.bytes + s2.bytes - 8.0 * (double)s.out.C * s.out.H * s.out.W;
+                if (hook) hook->after(stream, kname, bytes * b.N, (s.flops + s2.flops) * b.N);
+                ++si;
+                continue;
+            }
+            if (hook) hook->cancel();
+        }
         if (s.group >= 2 && (s.kind == S_GEMM || s.kind == S_DWPW)) {
             // a launch group (group_siblings): one grid if the parts run the same grouped kernel
             // instance at this batch, else the members one by one below

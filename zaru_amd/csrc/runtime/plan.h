@@ -62,6 +62,9 @@ struct Step {
     // launch grouping (group_siblings): the first step of a group of independent sibling steps
     // holds the group's size (>= 2) and the members follow it; 1 = launched alone, 0 = a member
     int group = 1;
+    // mark_inverted_residuals: 1 = this expand (S_GEMM) and the next step (S_DWPW, its only reader)
+    // may run as one launch (launch_ir), the expanded tensor never stored
+    int ir = 0;
 };
 
 struct PlanOutput {

@@ -197,7 +197,8 @@ struct DwPwParams {
 //   groups: sibling steps launched as one grid (plan.cpp group_siblings, kernels/group.h)
 //   dwgap: depthwise + global average pool in one launch (plan.cpp fuse_dw_gap)
 //   rt: row-task depthwise inside the LDS-DMA MFMA dwpw (dwpw_dma_body, RT > 0)
-enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_VRES, FORM_VSTORE, FORM_WS, FORM_GROUPS, FORM_DWGAP, FORM_RT, FORM_COUNT };
+//   ir: expand 1x1 + depthwise + projection in one launch (plan.cpp mark_inverted_residuals, ir.hip)
+enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_VRES, FORM_VSTORE, FORM_WS, FORM_GROUPS, FORM_DWGAP, FORM_RT, FORM_IR, FORM_COUNT };
 bool form_on(Form f);
 
 bool stem_supported(int cin, int k, int stride, int cout);
@@ -230,5 +231,8 @@ constexpr int ZR_GROUP_MAX = 4;  // steps per launch group
 const char *launch_gemm_group(const GemmParams *p, int n, hipStream_t s);
 const char *launch_dwpw_group(const DwPwParams *p, int n, hipStream_t s);
 const char *launch_dwpw_mfma_group(const DwPwParams *p, int n, hipStream_t s);
+// An expand 1x1 (e) and the depthwise + 1x1 step reading its output (d) in one launch (ir.hip);
+// nullptr when the shapes do not fit (the caller launches both).
+const char *launch_ir(const GemmParams &e, const DwPwParams &d, hipStream_t s);
 
 }  // namespace zr
