@@ -364,9 +364,11 @@ __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int 
             mask |= (iy >= 0 && iy < H && ix >= 0 && ix < W ? 1u : 0u) << (ky * K + kx);
         }
 
-    // row-task geometry (RT > 0): thread tid runs tasks tid * NRT + r of a chunk, all of one
-    // channel (SEGS % NRT == 0); per task the run index of its aligned window start in row ky = 0,
-    // the rows inside the image, and whether it is the first / last segment of its output row
+    // row-task geometry (RT > 0): thread tid runs NRT tasks of one channel (SEGS % NRT == 0), SPT
+    // threads per channel; its task r is segment r * SPT + tid % SPT, so the lanes of a wave read
+    // adjacent windows (8-byte reads of adjacent lanes RT * S floats apart: at RT = 2, S = 1 no two
+    // lanes of a half-wave share a bank).  Per task: the run index of its aligned window start in
+    // row ky = 0, the rows inside the image, and whether it is the first / last segment of its row
     constexpr int RTE = RT > 0 ? RT : 1;
     constexpr int PLx = DwPad<K, S>::L, OFF = PLx & 1;
     constexpr int WW = (RTE - 1) * S + K, PR = WW - RTE * S - PLx;  // window floats, right pad
@@ -374,7 +376,8 @@ __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int 
     constexpr int SEGS = BN / RTE, TASKS = DFKC * SEGS, NRT = TASKS > 256 ? TASKS / 256 : 1;
     static_assert(RT == 0 || (RT % 2 == 0 && BN % RT == 0 && SEGS % NRT == 0 && (TASKS <= 256 || TASKS % 256 == 0)),
                   "row-task layout");
-    const int rt_c = RT > 0 ? tid * NRT / SEGS : 0;
+    constexpr int SPT = SEGS / NRT;
+    const int rt_c = RT > 0 ? tid / SPT : 0, rt_g = tid % SPT;
     const bool rt_on = RT > 0 && tid * NRT < TASKS;
     int rt_base[NRT];
     uint32_t rt_vm[NRT];
@@ -383,7 +386,7 @@ __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int 
         if (tid < 16) reinterpret_cast<float4 *>(lds_all)[tid] = make_float4(0.f, 0.f, 0.f, 0.f);  // the zero rows
 #pragma unroll
         for (int r = 0; r < NRT; ++r) {
-            const int g = (tid * NRT + r) % SEGS;
+            const int g = r * SPT + rt_g;
             const int j = j0 + g * RT;
             rt_ok[r] = rt_on && j < G.ncols;
             const int jj = rt_ok[r] ? j : 0;
@@ -450,8 +453,7 @@ __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int 
                             for (int o = 0; o < RTE; ++o) a[o] = __builtin_fmaf(wr[ky * K + kx], x[OFF + o * S + kx], a[o]);
                     }
                     apply_act_n<RTE>(P.dw_act, a, [&](int) { return live ? kc + c : Cin - 1; });
-                    const int g = (tid * NRT + r) % SEGS;
-                    float *dst = sD + c * BN + g * RTE;
+                    float *dst = sD + c * BN + (r * SPT + rt_g) * RTE;
 #pragma unroll
                     for (int o = 0; o < RTE; o += 2)
                         *reinterpret_cast<float2 *>(dst + o) =
@@ -597,25 +599,34 @@ static int dfkc_for(int wgs, int cin) {
 // segments.  Needs the models' TF-style padding with W = OW * S (so a row's first / last segment
 // holds all of its padding) and an even R (8-byte aligned windows: even W and run starts).
 // the widest row task an instance is built for: DFKC * BN / 256, capped where the window and the
-// K^2 weights would cost occupancy next to the accumulators (5x5 at MTW = 1 and MTW >= 3: 2, else 8)
+// K^2 weights would cost occupancy next to the accumulators (5x5 at MTW = 1 and MTW >= 3: 2, else 8).
+// 5x5 at MTW = 2: 4 (the palm 48^2 blocks: 219 -> 210 us at 256 frames; an 8-wide task's lanes
+// read windows 32 B apart, 4-way bank conflicts; profiles/r05_layers/)
 constexpr int rt_hi(int K, int MTW, int r) {
-    return r < 2 ? 2 : (MTW == 1 && K == 5) || MTW >= 3 ? 2 : r > 8 ? 8 : r;
+    return r < 2 ? 2 : (MTW == 1 && K == 5) || MTW >= 3 ? 2 : K == 5 && MTW == 2 && r > 4 ? 4 : r > 8 ? 8 : r;
+}
+
+// A/B knob (bitwise neutral, like the form switches): ZARU_HIP_RT_CAP = the widest row task
+static int rt_cap() {
+    static const int v = [] {
+        const char *e = std::getenv("ZARU_HIP_RT_CAP");
+        return e ? (int)std::strtol(e, nullptr, 10) : 0;
+    }();
+    return v;
 }
 
 template <int K, int S>
 static int rt_for(const DwPwParams &p, int bn, int r_hi) {
     if (!form_on(FORM_RT) || p.pad_l != DwPad<K, S>::L || p.pad_t != DwPad<K, S>::L || p.in.W != p.OW * S) return 0;
     for (int r = r_hi; r >= 2 && r >= r_hi / 2; r /= 2)
-        if (p.OW % r == 0 && bn % r == 0) return r;
+        if ((rt_cap() < 2 || r <= rt_cap()) && p.OW % r == 0 && bn % r == 0) return r;
     return 0;
 }
 
 template <int K, int S, int WM, int MTW, int DFKC>
 static const char *dma_launch(const DwPwParams &p, dim3 grid, size_t lds, int nct, int runmax, int bufsz, hipStream_t s) {
     constexpr int BN = (4 / WM) * 32, RH = rt_hi(K, MTW, DFKC * BN / 256);
-    // (5x5 at BN = 128, MTW = 1 -- the hand network's 28^2 block: 4 two-wide tasks per thread
-    // measured slower than the per-output depthwise, 212 vs 197 us at 341 ROIs)
-    const int rt = MTW == 1 && K == 5 && BN == 128 ? 0 : rt_for<K, S>(p, BN, RH);
+    const int rt = rt_for<K, S>(p, BN, RH);
     if (rt == RH) {
         hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, DFKC, RH>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
         return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,%d,%d>", K, S, WM, MTW, DFKC, RH);
