@@ -46,7 +46,8 @@ SWITCHES = {
     "no_dwgap": "-dwgap",
     "no_rt": "-rt",
     "no_ir": "-ir",
-    "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws,-groups,-dwgap,-rt,-ir",
+    "no_irl": "-irl",
+    "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws,-groups,-dwgap,-rt,-ir,-irl",
 }
 
 
@@ -105,7 +106,8 @@ def test_nonsquare_full_plane_conv(forms):
 
 # The warp-specialized form runs only on launches with about a tile per CU or more (the hand
 # network's 14^2 / 7^2 blocks from ~940 ROIs): a batch of its own, with the launched kernels read
-# back from the session profile so the test knows the form ran.
+# back from the session profile so the test knows the form ran.  The fused low-resolution
+# inverted residual (irl) takes those blocks by default, so both sides run without it.
 WS_CHILD = r"""
 import sys, ctypes as C, numpy as np
 sys.path.insert(0, sys.argv[1])
@@ -125,7 +127,7 @@ np.savez(sys.argv[2], kernels=kernels, **{f"o{i}": o for i, o in enumerate(outs)
 
 def test_ws_form_is_bitwise_neutral(tmp_path):
     res = {}
-    for name, env in (("default", ""), ("no_ws", "-ws")):
+    for name, env in (("default", "-irl"), ("no_ws", "-irl,-ws")):
         path = str(tmp_path / f"{name}.npz")
         subprocess.run([sys.executable, "-c", WS_CHILD, REPO, path], env=dict(os.environ, ZARU_HIP_FORMS=env),
                        check=True, timeout=110)

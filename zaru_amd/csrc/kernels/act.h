@@ -51,4 +51,18 @@ __device__ __forceinline__ void apply_act_n(const Act &a, float *v, ChanFn ch) {
     }
 }
 
+// The activations the fused inverted-residual forms take (ir.hip / irl.hip, host-checked): Relu /
+// Clip / none, the same bounds on every channel, applied as min(max(v, lo), hi).  Bit for bit apply_act's result: Relu is max(v, 0)
+// (min with +inf keeps it), Clip is the same min(max()), and max(v, -inf) / min(v, +inf) leave a
+// finite v as it is.
+struct Bounds {
+    float lo, hi;
+};
+__device__ __forceinline__ Bounds bounds(const Act &a) {
+    const float inf = __builtin_inff();
+    return {a.kind == ACT_RELU ? 0.f : a.kind == ACT_CLIP ? a.lo : -inf, a.kind == ACT_CLIP ? a.hi : inf};
+}
+__device__ __forceinline__ float clamp(const Bounds &b, float v) { return fminf(fmaxf(v, b.lo), b.hi); }
+inline bool bounds_act(const Act &a) { return a.kind == ACT_NONE || a.kind == ACT_RELU || a.kind == ACT_CLIP; }
+
 }  // namespace zr

@@ -53,18 +53,6 @@ template <int K, int S> constexpr int ir_lrow() {
 }
 template <int K, int S> constexpr int ir_npw() { return ((ir_fp<K, S>() + 15) / 16 + 3) / 4; }
 
-// The activations this form takes (host-checked): Relu / Clip / none, the same bounds on every
-// channel, applied as min(max(v, lo), hi).  Bit for bit apply_act's result: Relu is max(v, 0)
-// (min with +inf keeps it), Clip is the same min(max()), and max(v, -inf) / min(v, +inf) leave a
-// finite v as it is.
-struct Bounds {
-    float lo, hi;
-};
-__device__ __forceinline__ Bounds bounds(const Act &a) {
-    const float inf = __builtin_inff();
-    return {a.kind == ACT_RELU ? 0.f : a.kind == ACT_CLIP ? a.lo : -inf, a.kind == ACT_CLIP ? a.hi : inf};
-}
-__device__ __forceinline__ float clamp(const Bounds &b, float v) { return fminf(fmaxf(v, b.lo), b.hi); }
 
 // E: the expand GEMM (x = block input, K = 16, M = Ce); D: the depthwise + projection step
 // (D.g.K = Ce, D.g.M = Cout <= CO, residual = the block input or its 2x2 max-pool)

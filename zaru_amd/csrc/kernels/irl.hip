@@ -1,0 +1,291 @@
+// irl.hip -- the MobileNetV2 inverted residual of the hand landmark network's low-resolution
+// blocks (14^2 planes with 288 / 384 expanded channels, 7^2 with 672) in one launch.  Reference:
+// the Conv / Clip / Add nodes of hand_landmark_lite.onnx that ORT / tract execute at
+// crates/zaru/src/nn/mod.rs:483-533 (hand/landmark.rs:251-322).
+//
+// Unfused, each of these blocks is an expand GEMM that writes 4-6x the block's channels to HBM
+// and a depthwise -> 1x1 launch that reads them back over 18-42 serial 16-channel chunks, with a
+// DMA round trip per chunk (profiles/r05_layers/: 170-190 us per block at 341 ROIs).  Here one
+// 512-thread workgroup owns one image's whole plane (196 or 49 positions) and walks the expanded
+// channels in chunks of 16 as a three-stage pipeline, one barrier per step:
+//   * waves 0-3 (one per SIMD) run the matrix work of step t: the expand of chunk t on f32 MFMA
+//     (v_mfma_f32_16x16x4f32; A = the chunk's 16 rows of the expand weights, loaded a step ahead;
+//     B = the block input, in registers for the whole launch) + bias, activation, into a
+//     zero-bordered padded plane in LDS (the border is the depthwise's zero padding, written
+//     once), then the projection of chunk t - 2 (v_mfma_f32_32x32x2f32 into registers; a wave
+//     owns one 32-row slice and every (4 / slices)-th 32-column tile);
+//   * waves 4-7 run the depthwise of chunk t - 1 beside them, as row tasks (RW adjacent outputs of
+//     one row of one channel: each of the K input rows read once, 8-byte LDS reads where rows are
+//     aligned; K^2 weights and the bias from LDS) into a [16][columns] tile, and stage chunk t's
+//     depthwise weights;
+//   * planes, tiles and weights are double-buffered by step parity; the barrier waits for LDS
+//     traffic only, so the next step's weight loads stay in flight.
+// Epilogue: epilogue_tile (bias, activation, residual, activation), as the unfused launches.
+//
+// Arithmetic and order are the unfused launches': the expand is an f32 MFMA chain over k in order
+// (16x16x4 and 32x32x2 both sum an output's products in k order like an fmaf chain --
+// tools/debug/mfma_order.hip, profiles/r04_mfma_order_probe.json) then + bias and the activation
+// (gemm_tiled_kernel's epilogue); the depthwise is bias + fmaf over the taps in (ky, kx) order
+// with the padding read as +0 (the masked taps' fmaf(w, 0, a)); the projection the same MFMA
+// chain over the expanded channels.  So fusing changes no output bit (tests/test_gpu_forms.py,
+// -irl).
+#include "../runtime/zr_kernels.h"
+#include "act.h"
+#include "epilogue.h"
+
+namespace zr {
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int IRL_CEC = 16;  // expanded channels per chunk
+
+// a workgroup barrier that waits for this wave's LDS traffic, not its vector-memory loads
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// HW: plane side (stride 1, 'same' padding); CX: block-input channels (the expand's K); MP: 32-row
+// slices of the projection (Mpad / 32)
+template <int K, int HW, int CX, int MP>
+__global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPwParams D) {
+    constexpr int P = HW * HW, PL = K / 2;
+    constexpr int PH = HW + K - 1, PW = (PH + 1) & ~1, PP = PH * PW;  // padded plane (even rows)
+    constexpr int NE = (P + 15) / 16, NEW = (NE + 3) / 4;              // expand column tiles (per M wave)
+    constexpr int NCT = (P + 31) / 32, NCP = NCT * 32;                // projection column tiles
+    constexpr int CPW = 4 / MP, TPW = (NCT + CPW - 1) / CPW;           // tile stride, tiles per M wave
+    constexpr int KS = CX / 4, KK = K * K, NSW = IRL_CEC * KK + IRL_CEC;
+    // depthwise task: RW outputs of a row (a half row when whole rows leave half the D threads idle)
+    constexpr int RW = IRL_CEC * HW * 2 <= 256 && HW % 2 == 0 ? HW / 2 : HW, RPR = HW / RW;
+    constexpr int WWIN = (RW + K - 1 + 1) & ~1;  // window floats per input row (even)
+    constexpr bool W64 = RW == HW;               // whole rows start 8-byte aligned: 8-byte reads
+    static_assert(4 % MP == 0 && CX % 4 == 0 && IRL_CEC * HW * RPR <= 256 && NE >= 4, "irl layout");
+    __shared__ __attribute__((aligned(16))) float sE[2][IRL_CEC * PP];  // expanded planes (zero border)
+    __shared__ __attribute__((aligned(16))) float sD[2][IRL_CEC * NCP];  // depthwise tiles
+    __shared__ float sW[2][NSW];  // a chunk's depthwise weights, then its biases
+
+    const GemmParams &G = D.g;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = blockIdx.x;
+    if (G.nact && n >= *G.nact) return;  // (whole workgroup, before any barrier)
+    const int nch = E.M / IRL_CEC;
+    const bool mrole = wave < 4;         // waves 0-3: MFMA (expand, projection); 4-7: depthwise
+
+    for (int i = tid; i < 2 * IRL_CEC * PP; i += 512) (&sE[0][0])[i] = 0.f;  // the borders stay 0
+
+    // ---- M waves: expand operands (lane (col, kq): x[4 s + kq][t * 16 + col] of tiles
+    // t = wave + 4 i as B; W1[c0 + col][4 s + kq] as A) and projection accumulators (32-row slice
+    // m0, column tiles ct0, ct0 + CPW, ...)
+    const int col = lane & 15, kq = lane >> 4;
+    const int mw = wave & 3;
+    const int m0 = (mw % MP) * 32, ct0 = mw / MP;
+    const int pcol = lane & 31, kh = lane >> 5;
+    float xr[NEW][KS];
+    f32x16 acc[TPW];
+    if (mrole) {
+        const float *xb = E.x + (size_t)(uint32_t)n * (uint32_t)E.x_sN;
+#pragma unroll
+        for (int i = 0; i < NEW; ++i) {
+            const int p = (mw + 4 * i) * 16 + col;
+            const uint32_t pc = p < P ? (uint32_t)p : 0u;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) xr[i][s] = xb[(uint32_t)(4 * s + kq) * (uint32_t)E.x_sC + pc];
+        }
+#pragma unroll
+        for (int i = 0; i < TPW; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+    }
+    const Bounds eb = bounds(E.pre), db = bounds(D.dw_act);  // (E.post: none, host-checked)
+
+    // M-wave operands, two steps ahead: set t & 1 holds the expand's A operands and biases of
+    // chunk t and the projection's A operands of chunk t - 2; each part is reloaded (for step t + 2)
+    // right after its last use in step t, into the same registers (a copy would wait for the
+    // loads), with chunk indices clamped past the ends
+    struct Ops {
+        float wa[KS], bias[4], w2[IRL_CEC / 2];
+    };
+    auto load_e = [&](int ce, Ops &o) {
+        const int c0 = (ce < nch ? ce : nch - 1) * IRL_CEC;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) o.wa[s] = E.wt[(uint32_t)(4 * s + kq) * (uint32_t)E.Mpad + (uint32_t)(c0 + col)];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o.bias[r] = E.bias[c0 + 4 * kq + r];
+    };
+    auto load_p = [&](int cp, Ops &o) {
+        const int c2 = (cp < 0 ? 0 : cp < nch ? cp : nch - 1) * IRL_CEC;
+#pragma unroll
+        for (int s = 0; s < IRL_CEC / 2; ++s)
+            o.w2[s] = G.wt[(uint32_t)(c2 + 2 * s + kh) * (uint32_t)G.Mpad + (uint32_t)(m0 + pcol)];
+    };
+
+    // ---- D waves: channel dc of a chunk, outputs dx0 .. dx0 + RW - 1 of row dy
+    const int dt = tid - 256;
+    const bool dw_on = !mrole && dt < IRL_CEC * HW * RPR;
+    const int dc = dw_on ? dt / (HW * RPR) : 0, dr = dt - dc * HW * RPR, dy = dr / RPR, dx0 = (dr - dy * RPR) * RW;
+    // chunk c's depthwise weights and biases: loaded a step ahead into registers (NSW <= 512:
+    // two words per D thread), stored to LDS in the step before their use
+    constexpr int NSR = (NSW + 255) / 256;
+    float swr[NSR];
+    auto load_w = [&](int c) {
+        c = c < nch ? c : nch - 1;
+#pragma unroll
+        for (int j = 0; j < NSR; ++j) {
+            const int i = dt + 256 * j;
+            swr[j] = i < IRL_CEC * KK ? D.dw_w[c * IRL_CEC * KK + i] : i < NSW ? D.dw_b[c * IRL_CEC + i - IRL_CEC * KK] : 0.f;
+        }
+    };
+
+    // Step t: the M waves expand chunk t into sE[t & 1] and project chunk t - 2 from sD[t & 1];
+    // the D waves run chunk t - 1's depthwise (sE[(t - 1) & 1] -> sD[(t - 1) & 1]) and stage chunk
+    // t's depthwise weights.  One barrier per step hands the buffers over.
+    auto step = [&](int t, Ops &o) {
+        if (mrole) {
+            if (t < nch) {
+                // expand; each tile's MFMA chain is issued before the previous tile's epilogue
+                float *pe = sE[t & 1];
+                auto chain = [&](int i) {
+                    f32x4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int s = 0; s < KS; ++s) d = __builtin_amdgcn_mfma_f32_16x16x4f32(o.wa[s], xr[i][s], d, 0, 0, 0);
+                    return d;
+                };
+                auto epi = [&](int i, const f32x4 &d) {  // gemm_tiled_kernel's epilogue (RES = false)
+                    const int p = (mw + 4 * i) * 16 + col;
+                    if (p < P) {
+                        const int y = p / HW, x = p - y * HW;
+                        float *e = pe + (4 * kq) * PP + (y + PL) * PW + x + PL;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) e[r * PP] = clamp(eb, d[r] + o.bias[r]);
+                    }
+                };
+                f32x4 dcur = chain(0);
+#pragma unroll
+                for (int i = 0; i < NEW; ++i) {
+                    f32x4 dn = dcur;
+                    if (i + 1 < NEW && mw + 4 * (i + 1) < NE) dn = chain(i + 1);
+                    if (mw + 4 * i < NE) epi(i, dcur);  // (wave-uniform)
+                    dcur = dn;
+                }
+                load_e(t + 2, o);
+            }
+            if (t >= 2) {
+                // projection: acc += W2[m0 .. m0 + 31][chunk t - 2] x its depthwise tile
+                const float *pd = sD[t & 1];
+#pragma unroll
+                for (int s = 0; s < IRL_CEC / 2; ++s) {
+                    const float *b = pd + (2 * s + kh) * NCP + pcol;
+#pragma unroll
+                    for (int i = 0; i < TPW; ++i) {
+                        const int ct = ct0 + CPW * i;
+                        if (ct < NCT) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(o.w2[s], b[ct * 32], acc[i], 0, 0, 0);
+                    }
+                }
+                load_p(t, o);
+            }
+        } else {
+            if (t < nch) {
+#pragma unroll
+                for (int j = 0; j < NSR; ++j)
+                    if (dt + 256 * j < NSW) sW[t & 1][dt + 256 * j] = swr[j];
+                load_w(t + 1);
+            }
+            if (t >= 1 && t <= nch && dw_on) {
+                // depthwise of chunk t - 1: RW outputs of one row of one channel, each input row once
+                const float *w = sW[(t - 1) & 1] + dc * KK;
+                const float *pe = sE[(t - 1) & 1] + dc * PP + dx0;
+                float a[RW];
+                const float bb = sW[(t - 1) & 1][IRL_CEC * KK + dc];
+#pragma unroll
+                for (int o = 0; o < RW; ++o) a[o] = bb;
+#pragma unroll
+                for (int ky = 0; ky < K; ++ky) {
+                    const float *row = pe + (dy + ky) * PW;
+                    float xw[WWIN];
+                    if constexpr (W64) {
+#pragma unroll
+                        for (int e = 0; e < WWIN / 2; ++e) {
+                            const float2 v = reinterpret_cast<const float2 *>(row)[e];
+                            xw[2 * e] = v.x;
+                            xw[2 * e + 1] = v.y;
+                        }
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < RW + K - 1; ++e) xw[e] = row[e];
+                    }
+#pragma unroll
+                    for (int kx = 0; kx < K; ++kx) {
+                        const float wt = w[ky * K + kx];
+#pragma unroll
+                        for (int o = 0; o < RW; ++o) a[o] = __builtin_fmaf(wt, xw[o + kx], a[o]);
+                    }
+                }
+                float *dst = sD[(t - 1) & 1] + dc * NCP + dy * HW + dx0;
+#pragma unroll
+                for (int o = 0; o < RW; ++o) dst[o] = clamp(db, a[o]);
+            }
+        }
+        lds_barrier();
+    };
+
+    Ops S0, S1;
+    if (mrole) {
+        load_e(0, S0);
+        load_p(0, S0);
+        load_e(1, S1);
+        load_p(1, S1);
+    } else {
+        load_w(0);
+    }
+    lds_barrier();  // the zeroed planes
+    for (int t = 0; t < nch + 2; t += 2) {  // (nch even, host-checked: set t & 1 is static)
+        step(t, S0);
+        step(t + 1, S1);
+    }
+
+    if (mrole) {
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+            const int ct = ct0 + CPW * i;
+            const int q = ct * 32 + pcol;
+            if (ct < NCT && q < P) {
+                // opaque row base / half: otherwise the compiler hoists every row's channel index
+                // and bias / residual address out of the step loop and holds them across it
+                int mb = m0, h = kh;
+                asm volatile("" : "+v"(mb), "+v"(h));
+                epilogue_tile(G, acc[i], n, q, mb, h);
+            }
+        }
+    }
+}
+
+template <int K, int HW, int CX, int MP>
+const char *irl_go(const GemmParams &e, const DwPwParams &d, hipStream_t s) {
+    const int N = d.g.ncols / (HW * HW);
+    hipLaunchKernelGGL((irl_kernel<K, HW, CX, MP>), dim3(N), dim3(512), 0, s, e, d);
+    return kernel_name("irl_kernel<%d,%d,%d,%d>", K, HW, CX, MP);
+}
+
+}  // namespace
+
+// The fused form applies to an expand (1x1, no residual, CNHW input) whose output only the next
+// depthwise -> 1x1 step reads (plan.cpp mark_inverted_residuals), at stride 1 with 'same'
+// padding over a 14^2 or 7^2 plane, with expanded channels in whole chunks of 16, Relu / Clip
+// activations on the expand and depthwise, and the hand network's (K, plane, input channels,
+// output rows) combinations.
+const char *launch_irl(const GemmParams &e, const DwPwParams &d, hipStream_t s) {
+    if (!form_on(FORM_IRL) || e.KK != 1 || e.res_mode != 0 || e.x_sN != e.P || e.M != d.g.K || e.M % IRL_CEC != 0 ||
+        e.out != d.in.p || e.nact != d.g.nact || d.stride != 1 || d.in.H != d.in.W || d.OW != d.in.W ||
+        d.g.P != d.in.H * d.in.W || e.P != d.g.P || d.in.sN != (int64_t)d.g.P || d.g.o_sP != 1 ||
+        d.g.ncols % d.g.P != 0 || e.ncols != d.g.ncols || d.pad_t != d.k / 2 || d.pad_l != d.k / 2 ||
+        d.g.res_mode == 2 || e.M % (2 * IRL_CEC) != 0 || e.post.kind != ACT_NONE || !bounds_act(e.pre) || !bounds_act(d.dw_act))
+        return nullptr;
+    const int hw = d.in.W, cx = e.K, mp = d.g.Mpad / 32;
+    if (d.g.Mpad % 32 != 0) return nullptr;
+    if (d.k == 3 && hw == 14 && cx == 48 && mp == 2) return irl_go<3, 14, 48, 2>(e, d, s);
+    if (d.k == 5 && hw == 14 && cx == 48 && mp == 2) return irl_go<5, 14, 48, 2>(e, d, s);
+    if (d.k == 5 && hw == 14 && cx == 64 && mp == 2) return irl_go<5, 14, 64, 2>(e, d, s);
+    if (d.k == 5 && hw == 7 && cx == 112 && mp == 4) return irl_go<5, 7, 112, 4>(e, d, s);
+    return nullptr;
+}
+
+}  // namespace zr

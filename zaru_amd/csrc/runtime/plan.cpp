@@ -1256,7 +1256,9 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook
             const GemmParams ge = gemm_of(s);
             const DwPwParams dp = dwpw_of(s2);
             if (hook) hook->before(stream);
-            if (const char *kname = launch_ir(ge, dp, stream)) {
+            const char *kname = launch_ir(ge, dp, stream);
+            if (!kname) kname = launch_irl(ge, dp, stream);
+            if (kname) {
                 // fused-boundary bytes: the block input (+ residual) and the output
                 const double bytes = s.bytes + s2.bytes - 8.0 * (double)s.out.C * s.out.H * s.out.W;
                 if (hook) hook->after(stream, kname, bytes * b.N, (s.flops + s2.flops) * b.N);
