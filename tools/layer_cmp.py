@@ -14,6 +14,12 @@ def load(path,reps=5):
         out.append((k,us))
     return out
 a=load(sys.argv[1]); b=load(sys.argv[2])
+if len(a)!=len(b):  # different launch lists (a fused form on one side): each list with its total
+    for name,l in (("A",a),("B",b)):
+        print(f"== {name}: {sys.argv[1] if name=='A' else sys.argv[2]}")
+        for k,us in l: print(f"{us:8.1f} {k}")
+        print(f"total {sum(u for _,u in l):.1f}  launches {len(l)}")
+    sys.exit(0)
 ta=tb=0
 for (ka,ua),(kb,ub) in zip(a,b):
     ta+=ua; tb+=ub
