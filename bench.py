@@ -46,6 +46,13 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+# Hardware queues per process (read by the HIP runtime at initialisation, so set before anything
+# here touches the GPU).  The face line runs 4 sub-batch streams + 1 gather stream; with HIP's
+# default of 4 queues, streams beyond that share a queue and independent sub-batches serialise
+# behind each other.  8 queues with 4 face sub-batches: 255.7 k vs 247.7-251.4 k faces/s with 4
+# queues and 3 (profiles/r05_hwqueues_ab.txt).  A value set by the caller is kept.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md chip table)
 FP32_PEAK_TFLOPS = 157.3   # f32 MFMA = f32 VALU peak
 METRIC = "end-to-end faces/sec (detect+468-pt mesh), 1080p synthetic, 1/2/4/8 GPU"
@@ -74,6 +81,13 @@ PIPELINE = {"face": ("face", "", ""), "hand": ("hand", "", ""),
             "face_next": ("face", "face_full", "facemesh_v2")}
 
 
+def sub_batches(args, kind):
+    """Sub-batches per step: --sub-batches, else 4 for the face line (with 8 hardware queues,
+    profiles/r05_hwqueues_ab.txt) and 3 for the others (the hand line's 341-ROI sub-batches:
+    91.8 k ROIs/s against 81.6 k with 4, profiles/r05_bench_hand_subbatches.txt)."""
+    return args.sub_batches or (4 if kind == "face" else 3)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -82,7 +96,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=1024, help="frames per step per GPU")
     ap.add_argument("--workload", choices=["face", "hand", "both", "face_next"], default="face")
     ap.add_argument("--threads", type=int, default=16, help="host decode/map threads per rank")
-    ap.add_argument("--sub-batches", type=int, default=3)
+    ap.add_argument("--sub-batches", type=int, default=None,
+                    help="software-pipelined sub-batches per step (default: face 4, others 3)")
     ap.add_argument("--streams", choices=["multi", "single"], default="multi")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -206,7 +221,7 @@ def measure_traffic(args, kind, batch=None):
              "--no-cpu-baseline", "--no-profile", "--no-traffic", "--no-hand", "--no-next", "--no-tracking",
              "--no-jpeg", "--no-c5"] + (["--host-post"] if args.host_post else []) + [
              "--batch", str(batch or args.batch), "--workload", kind,
-             "--sub-batches", str(args.sub_batches), "--streams", args.streams]
+             "--sub-batches", str(sub_batches(args, kind)), "--streams", args.streams]
     kib, launches = {}, {}
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     with tempfile.TemporaryDirectory(dir=os.path.join(REPO, "gpurun_out")) as d:
@@ -460,7 +475,7 @@ def main():
     threads = args.threads if len(kinds) == 1 else max(2, args.threads // 2)
     wls = []
     for k in kinds:  # config 5: the hand pipeline runs on the face pipeline's frames
-        wls.append(Workload(H, k, device, args.batch, rank, threads, args.sub_batches,
+        wls.append(Workload(H, k, device, args.batch, rank, threads, sub_batches(args, k),
                             args.streams == "multi", shared=wls[0] if wls else None))
     comms, gather = [], None
     if world > 1:
@@ -558,7 +573,8 @@ def main():
                                 "face_next": NEXT_WORKLOAD}[wl.kind]
                    + (" + config 4 hand pipeline concurrently on its own streams (config 5)" if len(wls) > 1 else ""),
                    "frames_per_gpu_per_step": args.batch, "frame": "1920x1080 RGBA8",
-                   "sub_batches": args.sub_batches, "streams": args.streams,
+                   "sub_batches": sub_batches(args, wl.kind), "streams": args.streams,
+                   "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                    "parallelism": f"frame-sharded x{world}"
                    + ((", device-written detection records copied to the host and all-gathered over gloo "
                        "each step (shared-GPU dry run: gloo has no device path)" if share
@@ -626,7 +642,7 @@ def next_line(H, args, device, traffic=None):
     """SURVEY §8f-1 on the same GPU after the face line: BlazeFace full range (192^2, 2304
     anchors) -> FaceMesh V2 (256^2, 478 points) over config 3's frame generator."""
     import torch
-    w = Workload(H, "face_next", device, args.next_batch, 0, args.threads, args.sub_batches,
+    w = Workload(H, "face_next", device, args.next_batch, 0, args.threads, sub_batches(args, "face_next"),
                  args.streams == "multi")
     run_steps([w], 5, None, 0, 1, None)
     torch.cuda.synchronize()
@@ -840,9 +856,9 @@ def c5_line(H, args, device, wl):
     import torch
     from concurrent.futures import ThreadPoolExecutor
     threads = max(2, args.threads // 2)
-    face = Workload(H, "face", device, args.batch, 0, threads, args.sub_batches, args.streams == "multi",
+    face = Workload(H, "face", device, args.batch, 0, threads, sub_batches(args, "face"), args.streams == "multi",
                     shared=wl)
-    hand = Workload(H, "hand", device, args.batch, 0, threads, args.sub_batches, args.streams == "multi",
+    hand = Workload(H, "hand", device, args.batch, 0, threads, sub_batches(args, "hand"), args.streams == "multi",
                     shared=wl)
     pool = ThreadPoolExecutor(2)
     prime([face, hand], 0.3, pool)
@@ -869,7 +885,7 @@ def hand_line(H, args, device, traffic=None):
     lite on 4 ROIs per frame (detection-derived when the palm detector fires, else seeded
     rotated ROIs).  The frames hold no hands, so the figure is landmark-ROI throughput."""
     import torch
-    w = Workload(H, "hand", device, args.hand_batch, 0, args.threads, args.sub_batches,
+    w = Workload(H, "hand", device, args.hand_batch, 0, args.threads, sub_batches(args, "hand"),
                  args.streams == "multi")
     run_steps([w], 5, None, 0, 1, None)
     torch.cuda.synchronize()
