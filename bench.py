@@ -593,6 +593,10 @@ def main():
                          "concurrent sub-batches (detector / decode+NMS+map+ROI seeding / landmark "
                          "network / tracker update)") if Workload.device_post else "host waits and host work",
         "host_wait_ms_per_step": round(times[0]["host_wait_ms"] / args.steps, 3),
+        # NMS candidates (confidence >= threshold) whose exact confidence another candidate of the
+        # frame shares: nms.rs:66's unstable sort pins their order only up to 20 candidates
+        "nms_ties": {"candidates": int(times[0]["nms_candidates"]), "tied": int(times[0]["nms_tied"]),
+                     "unpinned_frames": int(times[0]["nms_unpinned_frames"]), "frames": int(frames)},
         "pipeline_roofline": {
             "model": "SURVEY.md §8d: fixed algorithmic bytes per frame (detector + preprocessing + "
                      "landmark net per ROI), fp32 activations at layer boundaries",
