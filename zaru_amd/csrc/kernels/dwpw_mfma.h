@@ -511,18 +511,30 @@ __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int 
     if (j >= G.ncols) return;
     const int on = j / Pq, oq = j - on * Pq;
 #pragma unroll
-    for (int t = 0; t < MTW; ++t) epilogue_tile(G, acc[t], on, oq, m0 + (wm * MTW + t) * 32, kh);
+    for (int t = 0; t < MTW; ++t) {
+        // opaque row base / half: otherwise the compiler hoists every row's channel index and
+        // bias / residual address out of the chunk loop and holds them across it
+        int mb = m0 + (wm * MTW + t) * 32, h = kh;
+        asm volatile("" : "+v"(mb), "+v"(h));
+        epilogue_tile(G, acc[t], on, oq, mb, h);
+    }
 }
 
+// 4 waves per SIMD (<= 128 VGPRs) where the layout fits them: MTW = 1, and MTW = 2 at 3x3
+// (BlazeFace's 16^2 blocks 48.6 -> 46.0 us at 341 images; the palm's 5x5 MTW-2 layouts measured
+// 1-5 % slower at 4 waves, with 2-53 spilled registers: profiles/r05_layers/)
+template <int K, int WM, int MTW> constexpr int dma_waves(int rt) {
+    return MTW == 1 || (MTW == 2 && K == 3) ? 4 : rt > 0 ? 2 : 1;
+}
 template <int K, int S, int WM, int MTW, int DFKC, int RT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTW == 1 ? 4 : RT > 0 ? 2 : 1)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_waves<K, WM, MTW>(RT))))
 void dwpw_dma_kernel(const DwPwParams P, int nct, int runmax, int bufsz) {
     dwpw_dma_body<K, S, WM, MTW, DFKC, RT>(P, nct, runmax, bufsz, blockIdx.x, blockIdx.y, gridDim.x);
 }
 
 // sibling layers in one launch (group.h): a0 = nct, a1 = runmax, a2 = bufsz of each part
 template <int K, int S, int WM, int MTW, int DFKC, int RT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTW == 1 ? 4 : RT > 0 ? 2 : 1)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_waves<K, WM, MTW>(RT))))
 void dwpw_dma_group_kernel(const LaunchGroup<DwPwParams> G) {
     const GroupSlot t = group_slot(G);
     dwpw_dma_body<K, S, WM, MTW, DFKC, RT>(G.p[t.g], G.a0[t.g], G.a1[t.g], G.a2[t.g], t.bx, t.by, G.gx[t.g]);
