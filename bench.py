@@ -48,10 +48,11 @@ sys.path.insert(0, REPO)
 
 # Hardware queues per process (read by the HIP runtime at initialisation, so set before anything
 # here touches the GPU).  The face line runs 4 sub-batch streams + 1 gather stream; with HIP's
-# default of 4 queues, streams beyond that share a queue and independent sub-batches serialise
-# behind each other.  8 queues with 4 face sub-batches: 255.7 k vs 247.7-251.4 k faces/s with 4
-# queues and 3 (profiles/r05_hwqueues_ab.txt).  A value set by the caller is kept.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# default of 4 queues (which the GPU boxes also export), streams beyond that share a queue and
+# independent sub-batches serialise behind each other.  8 queues with 4 face sub-batches:
+# 255.7 k vs 247.7-251.4 k faces/s with 4 queues and 3, and 216-218 k with 4 queues and 4
+# (profiles/r05_hwqueues_ab.txt).  ZARU_BENCH_HW_QUEUES picks another count for A/B runs.
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("ZARU_BENCH_HW_QUEUES", "8")
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md chip table)
 FP32_PEAK_TFLOPS = 157.3   # f32 MFMA = f32 VALU peak
@@ -85,7 +86,9 @@ def sub_batches(args, kind):
     """Sub-batches per step: --sub-batches, else 4 for the face line (with 8 hardware queues,
     profiles/r05_hwqueues_ab.txt) and 3 for the others (the hand line's 341-ROI sub-batches:
     91.8 k ROIs/s against 81.6 k with 4, profiles/r05_bench_hand_subbatches.txt)."""
-    return args.sub_batches or (4 if kind == "face" else 3)
+    if args.sub_batches:
+        return args.sub_batches
+    return 4 if kind == "face" and int(os.environ["GPU_MAX_HW_QUEUES"]) >= 8 else 3
 
 
 def parse():
