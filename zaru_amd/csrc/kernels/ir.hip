@@ -236,8 +236,8 @@ const char *ir_go(const GemmParams &e, const DwPwParams &d, hipStream_t s) {
 
 // The fused form applies to an expand (1x1, 16 input channels, no residual, CNHW input) whose
 // output only the next depthwise -> 1x1 step reads (plan.cpp mark_inverted_residuals), with the
-// models' TF-style pads, W = OW * S, <= 32 output channels and the 3x3 s1 / s2 shapes of the hand
-// network's 112^2 and 56^2 blocks.
+// models' TF-style pads, W = OW * S, <= 32 output channels and the 3x3 s1 / s2 and 5x5 s2 shapes of
+// the hand network's 112^2 and 56^2 blocks.
 const char *launch_ir(const GemmParams &e, const DwPwParams &d, hipStream_t s) {
     if (!form_on(FORM_IR) || e.K != IR_CX || e.KK != 1 || e.res_mode != 0 || e.x_sN != e.P || e.M != d.g.K ||
         e.out != d.in.p || d.in.sN != (int64_t)d.in.H * d.in.W || d.g.M > 32 || d.g.o_sP != 1 ||
@@ -258,7 +258,10 @@ const char *launch_ir(const GemmParams &e, const DwPwParams &d, hipStream_t s) {
     const bool co16 = d.g.M <= 16;
     if (d.k == 3 && d.stride == 1) return co16 ? ir_go<3, 1, 16>(e, d, s) : ir_go<3, 1, 32>(e, d, s);
     if (d.k == 3 && d.stride == 2) return co16 ? ir_go<3, 2, 16>(e, d, s) : ir_go<3, 2, 32>(e, d, s);
-    return nullptr;  // (5x5 s2, 56^2 -> 28^2: measured slower fused, 393 vs 348 us at 341 ROIs)
+    // 5x5 s2 (56^2 -> 28^2): one workgroup per CU (83 KB of LDS), still 328 vs 352 us unfused at
+    // 341 ROIs (profiles/r05_layers/hand_landmark_lite_341_ir5_vs_unfused.txt)
+    if (d.k == 5 && d.stride == 2) return co16 ? ir_go<5, 2, 16>(e, d, s) : ir_go<5, 2, 32>(e, d, s);
+    return nullptr;
 }
 
 }  // namespace zr
