@@ -41,6 +41,24 @@ def test_plan_compiles_and_fuses(models_dir, model, launches):
     assert not [l for l in steps if l.startswith("elt")]
 
 
+@pytest.mark.parametrize("model,pairs", [
+    ("hand_landmark_lite", 14), ("face_detection_short_range", 0), ("face_landmark", 0),
+    ("palm_detection_lite", 0)])
+def test_inverted_residual_pairs(models_dir, model, pairs):
+    """mark_inverted_residuals: an expand 1x1 (gemm) is marked (ir=1) exactly when the next step is
+    the depthwise -> 1x1 that is the only reader of its output (the fused ir / irl launches)."""
+    txt = _lib.plan_describe(open(os.path.join(models_dir, model + ".onnx"), "rb").read())
+    steps = [dict(kv.split("=", 1) for kv in l.split() if "=" in kv) | {"kind": l.split()[0]}
+             for l in txt.splitlines() if l.split(" ")[0] in KINDS]
+    marked = [i for i, s in enumerate(steps) if s["ir"] == "1"]
+    assert len(marked) == pairs
+    for i in marked:
+        e, d = steps[i], steps[i + 1]
+        assert e["kind"] == "gemm" and d["kind"] == "dwpw" and d["in"] == e["out"]
+        readers = [s for s in steps if s["in"] == e["out"] or s.get("in2") == e["out"]]
+        assert readers == [d]
+
+
 @pytest.mark.parametrize("model,outputs", [
     ("face_detection_full_range", ["reshaped_regressor_face_4", "reshaped_classifier_face_4"]),
     ("face_landmarks_detector", None),

@@ -420,11 +420,12 @@ int zr_plan_describe(const uint8_t *onnx, size_t len, const uint32_t *out_sel, s
         }
         for (auto &st : plan.steps) {
             snprintf(line, sizeof line,
-                     "%s%s in=%s out=%s k=%dx%d s=%d M=%d K=%d KK=%d pre=%s post=%s res=%d rC=%d elt=%d off=%lld oN=%lld oC=%lld oP=%lld in2=%s grp=%d\n",
+                     "%s%s in=%s out=%s k=%dx%d s=%d M=%d K=%d KK=%d pre=%s post=%s res=%d rC=%d elt=%d off=%lld oN=%lld oC=%lld oP=%lld in2=%s grp=%d ir=%d\n",
                      kinds[st.kind], st.stem ? " stem" : "", ref(st.in).c_str(), ref(st.out).c_str(), st.kh, st.kw, st.stride,
                      st.M, st.K, st.KK, acts[st.pre.kind], acts[st.post.kind], st.res_mode, st.r_C,
                      st.elt_op, (long long)st.out.off, (long long)st.out.o_sN, (long long)st.out.o_sC,
-                     (long long)st.out.o_sP, (st.res_mode || st.kind == zr::S_ELT) ? ref(st.in2).c_str() : "-", st.group);
+                     (long long)st.out.o_sP, (st.res_mode || st.kind == zr::S_ELT) ? ref(st.in2).c_str() : "-", st.group,
+                     st.ir);
             t += line;
         }
         if (needed) *needed = t.size() + 1;
