@@ -1,6 +1,11 @@
 // dwpw_mfma.hip -- layout choice and launch of the MFMA dwpw forms (dwpw_mfma.h), and the grouped
 // launches of sibling layers.  Reference: the Conv nodes of the four ONNX graphs that ORT/tract
 // execute at crates/zaru/src/nn/mod.rs:483-533 (the BlazeBlocks).
+#include <array>
+#include <map>
+#include <mutex>
+#include <vector>
+
 #include "dwpw_mfma.h"
 
 namespace zr {
@@ -50,11 +55,75 @@ static const DwPwLayout *choose_layout(const DwPwParams &p) {
     return best;
 }
 
+static const char *launch_layout(const DwPwParams &p, const DwPwLayout &l, hipStream_t s) {
+    if (p.k == 3) return p.stride == 1 ? dwpw_layout_k3s1(p, l, s) : dwpw_layout_k3s2(p, l, s);
+    return p.stride == 1 ? dwpw_layout_k5s1(p, l, s) : dwpw_layout_k5s2(p, l, s);
+}
+
+// Layout tuning (ZARU_HIP_TUNE=1): the layouts compute the same arithmetic in the same order
+// (tests/test_gpu_forms.py), so which one runs is only a question of time.  The first launch of
+// a layer shape (kernel, stride, planes, channels, batch columns) times every admissible layout
+// on the launch's own stream (best of 3), and later launches of that shape take the fastest.
+static bool tune_on() {
+    static const bool v = [] {
+        const char *e = std::getenv("ZARU_HIP_TUNE");
+        return e && *e == '1';
+    }();
+    return v;
+}
+
+static const DwPwLayout *tuned_layout(const DwPwParams &p, hipStream_t s) {
+    typedef std::array<int64_t, 10> Key;
+    static std::mutex mu;
+    static std::map<Key, int> cache;
+    const Key key{p.k, p.stride, p.in.H, p.in.W, p.OW, p.g.K, p.g.M, p.g.Mpad, p.g.ncols, p.g.res_mode};
+    {
+        std::lock_guard<std::mutex> g(mu);
+        const auto it = cache.find(key);
+        if (it != cache.end()) return &kLayouts[it->second];
+    }
+    std::vector<int> cand;
+    for (int i = 0; i < (int)(sizeof(kLayouts) / sizeof(kLayouts[0])); ++i) {
+        const DwPwLayout &l = kLayouts[i];
+        const int mb = (p.g.Mpad + l.bm() - 1) / l.bm();
+        if (mb > 1 && l.bm() < 256) continue;
+        if ((int64_t)mb * l.bm() * 3 > (int64_t)p.g.Mpad * 4 && p.g.Mpad <= 256) continue;
+        cand.push_back(i);
+    }
+    const DwPwLayout *h = choose_layout(p);
+    int best = (int)(h - kLayouts);
+    if (cand.size() > 1) {
+        hipEvent_t e0, e1;
+        if (hipEventCreate(&e0) != hipSuccess) return h;
+        if (hipEventCreate(&e1) != hipSuccess) {
+            (void)hipEventDestroy(e0);
+            return h;
+        }
+        float tbest = 1e30f;
+        for (int rep = 0; rep < 3; ++rep)
+            for (int i : cand) {
+                if (hipEventRecord(e0, s) != hipSuccess) continue;
+                launch_layout(p, kLayouts[i], s);
+                if (hipEventRecord(e1, s) != hipSuccess) continue;
+                float ms = 0.f;
+                if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) continue;
+                if (ms < tbest) {
+                    tbest = ms;
+                    best = i;
+                }
+            }
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    }
+    std::lock_guard<std::mutex> g(mu);
+    cache.emplace(key, best);
+    return &kLayouts[best];
+}
+
 const char *launch_dwpw_mfma(const DwPwParams &p, hipStream_t s) {
     if (const char *k = launch_dwpw_ws(p, s, true)) return k;
-    const DwPwLayout *best = choose_layout(p);
-    if (p.k == 3) return p.stride == 1 ? dwpw_layout_k3s1(p, *best, s) : dwpw_layout_k3s2(p, *best, s);
-    return p.stride == 1 ? dwpw_layout_k5s1(p, *best, s) : dwpw_layout_k5s2(p, *best, s);
+    const DwPwLayout *best = tune_on() ? tuned_layout(p, s) : choose_layout(p);
+    return launch_layout(p, *best, s);
 }
 
 namespace {
