@@ -14,10 +14,13 @@ post-processing options of Detector (crates/zaru/src/detection.rs:44-111,186-202
 
 Palm detections on noise frames need a low threshold (Detector::set_threshold): at 0.05 the oracle
 puts 33-76 anchors of such frames above it, which exercises grouping, ordering and capacity."""
+import os
+
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 W, H, NF = 1920, 1080, 6
 
@@ -100,20 +103,34 @@ def test_records_world_must_match_the_communicator(frames):
     comm.close()
 
 
+PENDING_CHILD = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+from zaru_amd._lib import Comm, DeviceBuffer, ZaruError, lib, synchronize
+comm = Comm(Comm.unique_id(), 1, 0, 0)
+src, dst = DeviceBuffer(256), DeviceBuffer(256)
+# a HIP call of the library's own runtime that fails (pitch < width): its error is now pending
+assert lib().zr_memcpy2d_async(dst.ptr, 4, src.ptr, 256, 256, 1, 2, None) == -3
+try:
+    comm.all_gather_async(src.ptr, dst.ptr, 256)
+    raise SystemExit("the pending error was not reported")
+except ZaruError as e:
+    assert "pending HIP error" in str(e) and e.code == -3, (str(e), e.code)
+comm.all_gather_async(src.ptr, dst.ptr, 256)  # taken once: the next call runs
+synchronize()
+comm.close()
+print("pending error reported once")
+"""
+
+
 def test_comm_reports_a_pending_hip_error():
-    from zaru_amd._lib import Comm, DeviceBuffer, ZaruError
-    comm = Comm(Comm.unique_id(), 1, 0, 0)
-    src, dst = DeviceBuffer(256), DeviceBuffer(256)
-    # a HIP call of the library's own runtime that fails (pitch < width): its error is now pending
-    from zaru_amd._lib import lib
-    assert lib().zr_memcpy2d_async(dst.ptr, 4, src.ptr, 256, 256, 1, 2, None) == -3
-    with pytest.raises(ZaruError, match="pending HIP error") as e:
-        comm.all_gather_async(src.ptr, dst.ptr, 256)
-    assert e.value.code == -3
-    comm.all_gather_async(src.ptr, dst.ptr, 256)  # taken once: the next call runs
-    from zaru_amd._lib import synchronize
-    synchronize()
-    comm.close()
+    # in a process of its own: the deliberately failed HIP call must not leave runtime state
+    # behind for the tests that follow (one full-suite run saw a later pipeline check report an
+    # unrelated stale runtime error right after this test)
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, "-c", PENDING_CHILD, REPO], capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "reported once" in r.stdout, (r.stdout[-1000:], r.stderr[-2000:])
 
 
 def test_nms_remove_device_equals_host(frames):
