@@ -44,21 +44,21 @@ constexpr int IRL_CEC = 16;  // expanded channels per chunk
 // a workgroup barrier that waits for this wave's LDS traffic, not its vector-memory loads
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// HW: plane side (stride 1, 'same' padding); CX: block-input channels (the expand's K); MP: 32-row
-// slices of the projection (Mpad / 32)
-template <int K, int HW, int CX, int MP>
+// HW: input plane side; S: the depthwise stride (TF-style 'same' padding: the output plane is
+// HW / S); CX: block-input channels (the expand's K); MP: 32-row slices of the projection (Mpad / 32)
+template <int K, int HW, int S, int CX, int MP>
 __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPwParams D) {
-    constexpr int P = HW * HW, PL = K / 2;
-    constexpr int PH = HW + K - 1, PW = (PH + 1) & ~1, PP = PH * PW;  // padded plane (even rows)
-    constexpr int NE = (P + 15) / 16, NEW = (NE + 3) / 4;              // expand column tiles (per M wave)
-    constexpr int NCT = (P + 31) / 32, NCP = NCT * 32;                // projection column tiles
+    constexpr int HO = HW / S, P = HW * HW, PO = HO * HO, PL = S == 1 ? K / 2 : K / 2 - 1;
+    constexpr int PH = (HO - 1) * S + K, PW = (PH + 1) & ~1, PP = PH * PW;  // padded plane (even rows)
+    constexpr int NE = (P + 15) / 16, NEW = (NE + 3) / 4;                    // expand column tiles (per M wave)
+    constexpr int NCT = (PO + 31) / 32, NCP = NCT * 32;                     // projection column tiles
     constexpr int CPW = 4 / MP, TPW = (NCT + CPW - 1) / CPW;           // tile stride, tiles per M wave
     constexpr int KS = CX / 4, KK = K * K, NSW = IRL_CEC * KK + IRL_CEC;
     // depthwise task: RW outputs of a row (a half row when whole rows leave half the D threads idle)
-    constexpr int RW = IRL_CEC * HW * 2 <= 256 && HW % 2 == 0 ? HW / 2 : HW, RPR = HW / RW;
-    constexpr int WWIN = (RW + K - 1 + 1) & ~1;  // window floats per input row (even)
-    constexpr bool W64 = RW == HW;               // whole rows start 8-byte aligned: 8-byte reads
-    static_assert(4 % MP == 0 && CX % 4 == 0 && IRL_CEC * HW * RPR <= 256 && NE >= 4, "irl layout");
+    constexpr int RW = IRL_CEC * HO * 2 <= 256 && HO % 2 == 0 ? HO / 2 : HO, RPR = HO / RW;
+    constexpr int WWIN = ((RW - 1) * S + K + 1) & ~1;  // window floats per input row (even)
+    constexpr bool W64 = RW == HO || S == 2;           // 8-byte aligned window starts: 8-byte reads
+    static_assert(4 % MP == 0 && CX % 4 == 0 && IRL_CEC * HO * RPR <= 256 && NE >= 4 && HW % S == 0, "irl layout");
     __shared__ __attribute__((aligned(16))) float sE[2][IRL_CEC * PP];  // expanded planes (zero border)
     __shared__ __attribute__((aligned(16))) float sD[2][IRL_CEC * NCP];  // depthwise tiles
     __shared__ float sW[2][NSW];  // a chunk's depthwise weights, then its biases
@@ -120,8 +120,8 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
 
     // ---- D waves: channel dc of a chunk, outputs dx0 .. dx0 + RW - 1 of row dy
     const int dt = tid - 256;
-    const bool dw_on = !mrole && dt < IRL_CEC * HW * RPR;
-    const int dc = dw_on ? dt / (HW * RPR) : 0, dr = dt - dc * HW * RPR, dy = dr / RPR, dx0 = (dr - dy * RPR) * RW;
+    const bool dw_on = !mrole && dt < IRL_CEC * HO * RPR;
+    const int dc = dw_on ? dt / (HO * RPR) : 0, dr = dt - dc * HO * RPR, dy = dr / RPR, dx0 = (dr - dy * RPR) * RW;
     // chunk c's depthwise weights and biases: loaded a step ahead into registers (NSW <= 512:
     // two words per D thread), stored to LDS in the step before their use
     constexpr int NSR = (NSW + 255) / 256;
@@ -192,14 +192,14 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
             if (t >= 1 && t <= nch && dw_on) {
                 // depthwise of chunk t - 1: RW outputs of one row of one channel, each input row once
                 const float *w = sW[(t - 1) & 1] + dc * KK;
-                const float *pe = sE[(t - 1) & 1] + dc * PP + dx0;
+                const float *pe = sE[(t - 1) & 1] + dc * PP + dx0 * S;
                 float a[RW];
                 const float bb = sW[(t - 1) & 1][IRL_CEC * KK + dc];
 #pragma unroll
                 for (int o = 0; o < RW; ++o) a[o] = bb;
 #pragma unroll
                 for (int ky = 0; ky < K; ++ky) {
-                    const float *row = pe + (dy + ky) * PW;
+                    const float *row = pe + (dy * S + ky) * PW;
                     float xw[WWIN];
                     if constexpr (W64) {
 #pragma unroll
@@ -210,16 +210,16 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
                         }
                     } else {
 #pragma unroll
-                        for (int e = 0; e < RW + K - 1; ++e) xw[e] = row[e];
+                        for (int e = 0; e < (RW - 1) * S + K; ++e) xw[e] = row[e];
                     }
 #pragma unroll
                     for (int kx = 0; kx < K; ++kx) {
                         const float wt = w[ky * K + kx];
 #pragma unroll
-                        for (int o = 0; o < RW; ++o) a[o] = __builtin_fmaf(wt, xw[o + kx], a[o]);
+                        for (int o = 0; o < RW; ++o) a[o] = __builtin_fmaf(wt, xw[o * S + kx], a[o]);
                     }
                 }
-                float *dst = sD[(t - 1) & 1] + dc * NCP + dy * HW + dx0;
+                float *dst = sD[(t - 1) & 1] + dc * NCP + dy * HO + dx0;
 #pragma unroll
                 for (int o = 0; o < RW; ++o) dst[o] = clamp(db, a[o]);
             }
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
         for (int i = 0; i < TPW; ++i) {
             const int ct = ct0 + CPW * i;
             const int q = ct * 32 + pcol;
-            if (ct < NCT && q < P) {
+            if (ct < NCT && q < PO) {
                 // opaque row base / half: otherwise the compiler hoists every row's channel index
                 // and bias / residual address out of the step loop and holds them across it
                 int mb = m0, h = kh;
@@ -258,33 +258,36 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
     }
 }
 
-template <int K, int HW, int CX, int MP>
+template <int K, int HW, int S, int CX, int MP>
 const char *irl_go(const GemmParams &e, const DwPwParams &d, hipStream_t s) {
-    const int N = d.g.ncols / (HW * HW);
-    hipLaunchKernelGGL((irl_kernel<K, HW, CX, MP>), dim3(N), dim3(512), 0, s, e, d);
-    return kernel_name("irl_kernel<%d,%d,%d,%d>", K, HW, CX, MP);
+    const int N = d.g.ncols / ((HW / S) * (HW / S));
+    hipLaunchKernelGGL((irl_kernel<K, HW, S, CX, MP>), dim3(N), dim3(512), 0, s, e, d);
+    return kernel_name("irl_kernel<%d,%d,%d,%d,%d>", K, HW, S, CX, MP);
 }
 
 }  // namespace
 
 // The fused form applies to an expand (1x1, no residual, CNHW input) whose output only the next
-// depthwise -> 1x1 step reads (plan.cpp mark_inverted_residuals), at stride 1 with 'same'
-// padding over a 14^2 or 7^2 plane, with expanded channels in whole chunks of 16, Relu / Clip
-// activations on the expand and depthwise, and the hand network's (K, plane, input channels,
-// output rows) combinations.
+// depthwise -> 1x1 step reads (plan.cpp mark_inverted_residuals), with the models' TF-style
+// 'same' padding over a 14^2 or 7^2 plane (stride 1, or stride 2 from 14^2 to 7^2), with
+// expanded channels in whole chunks of 16, Relu / Clip activations on the expand and depthwise,
+// and the hand network's (K, plane, stride, input channels, output rows) combinations.
 const char *launch_irl(const GemmParams &e, const DwPwParams &d, hipStream_t s) {
+    const int S = d.stride, pl = S == 1 ? d.k / 2 : d.k / 2 - 1;
     if (!form_on(FORM_IRL) || e.KK != 1 || e.res_mode != 0 || e.x_sN != e.P || e.M != d.g.K || e.M % IRL_CEC != 0 ||
-        e.out != d.in.p || e.nact != d.g.nact || d.stride != 1 || d.in.H != d.in.W || d.OW != d.in.W ||
-        d.g.P != d.in.H * d.in.W || e.P != d.g.P || d.in.sN != (int64_t)d.g.P || d.g.o_sP != 1 ||
-        d.g.ncols % d.g.P != 0 || e.ncols != d.g.ncols || d.pad_t != d.k / 2 || d.pad_l != d.k / 2 ||
-        d.g.res_mode == 2 || e.M % (2 * IRL_CEC) != 0 || e.post.kind != ACT_NONE || !bounds_act(e.pre) || !bounds_act(d.dw_act))
+        e.out != d.in.p || e.nact != d.g.nact || (S != 1 && S != 2) || d.in.H != d.in.W || d.in.W % S != 0 ||
+        d.OW * S != d.in.W || d.g.P != d.OW * d.OW || e.P != d.in.H * d.in.W || d.in.sN != (int64_t)e.P ||
+        d.g.o_sP != 1 || d.g.ncols % d.g.P != 0 || e.ncols != d.in.H * d.in.W * (d.g.ncols / d.g.P) ||
+        d.pad_t != pl || d.pad_l != pl || d.g.res_mode == 2 || (d.g.res_mode == 1 && S != 1) ||
+        e.M % (2 * IRL_CEC) != 0 || e.post.kind != ACT_NONE || !bounds_act(e.pre) || !bounds_act(d.dw_act))
         return nullptr;
     const int hw = d.in.W, cx = e.K, mp = d.g.Mpad / 32;
     if (d.g.Mpad % 32 != 0) return nullptr;
-    if (d.k == 3 && hw == 14 && cx == 48 && mp == 2) return irl_go<3, 14, 48, 2>(e, d, s);
-    if (d.k == 5 && hw == 14 && cx == 48 && mp == 2) return irl_go<5, 14, 48, 2>(e, d, s);
-    if (d.k == 5 && hw == 14 && cx == 64 && mp == 2) return irl_go<5, 14, 64, 2>(e, d, s);
-    if (d.k == 5 && hw == 7 && cx == 112 && mp == 4) return irl_go<5, 7, 112, 4>(e, d, s);
+    if (S == 1 && d.k == 3 && hw == 14 && cx == 48 && mp == 2) return irl_go<3, 14, 1, 48, 2>(e, d, s);
+    if (S == 1 && d.k == 5 && hw == 14 && cx == 48 && mp == 2) return irl_go<5, 14, 1, 48, 2>(e, d, s);
+    if (S == 1 && d.k == 5 && hw == 14 && cx == 64 && mp == 2) return irl_go<5, 14, 1, 64, 2>(e, d, s);
+    if (S == 1 && d.k == 5 && hw == 7 && cx == 112 && mp == 4) return irl_go<5, 7, 1, 112, 4>(e, d, s);
+    if (S == 2 && d.k == 5 && hw == 14 && cx == 64 && mp == 4) return irl_go<5, 14, 2, 64, 4>(e, d, s);
     return nullptr;
 }
 
