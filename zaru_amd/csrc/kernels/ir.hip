@@ -223,8 +223,13 @@ template <int K, int S, int CO>
 const char *ir_go(const GemmParams &e, const DwPwParams &d, hipStream_t s) {
     constexpr int LP = ((IR_TH - 1) * S + K) * ir_lrow<K, S>();
     const size_t lds = sizeof(float) * IR_CEC * LP;
-    static const bool attr = hipFuncSetAttribute((const void *)ir_kernel<K, S, CO>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    static const bool attr = [] {
+        if (hipFuncSetAttribute((const void *)ir_kernel<K, S, CO>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) == hipSuccess)
+            return true;
+        (void)hipGetLastError();  // handled: the pair then runs unfused
+        return false;
+    }();
     if (!attr) return nullptr;
     const int OH = d.g.P / d.OW, tiles_x = (d.OW + IR_TW - 1) / IR_TW, tiles_y = (OH + IR_TH - 1) / IR_TH;
     const int N = d.g.ncols / d.g.P;
