@@ -181,3 +181,40 @@ def test_rt_form_is_bitwise_neutral_at_bench_batches(tmp_path):
     for k in res["default"]:
         if k != "kernels":
             assert np.array_equal(res["default"][k], res["no_rt"][k]), (k, float(np.abs(res["default"][k] - res["no_rt"][k]).max()))
+
+
+# Two images per workgroup at 7^2 (form "irl2", irl_kernel NI = 2) applies once the ROIs
+# outnumber the CUs: 341 (odd: the last workgroup's second image is past the end) and 1024.
+IRL2_CHILD = r"""
+import sys, ctypes as C, numpy as np
+sys.path.insert(0, sys.argv[1])
+from zaru_amd.nn import NeuralNetwork, model_bytes
+from zaru_amd._lib import lib, check
+out, kernels = {}, []
+net = NeuralNetwork.from_onnx(model_bytes("hand_landmark_lite")).load()
+check(lib().zr_profile_enable(net._h, 1))
+for b in (341, 1024):
+    x = np.random.default_rng(b).uniform(-1.0, 1.0, size=(b, 3, 224, 224)).astype(np.float32)
+    for i, o in enumerate(net.estimate(x)):
+        out[f"{b}/{i}"] = o
+need = C.c_size_t()
+buf = C.create_string_buffer(1 << 20)
+check(lib().zr_profile_read(net._h, buf, len(buf), C.byref(need)))
+kernels += [l.split()[0] for l in buf.value.decode().splitlines() if l.strip()]
+np.savez(sys.argv[2], kernels=np.array(kernels), **out)
+"""
+
+
+def test_irl2_form_is_bitwise_neutral(tmp_path):
+    res = {}
+    for name, env in (("default", ""), ("no_irl2", "-irl2")):
+        path = str(tmp_path / f"{name}.npz")
+        subprocess.run([sys.executable, "-c", IRL2_CHILD, REPO, path], env=dict(os.environ, ZARU_HIP_FORMS=env),
+                       check=True, timeout=110)
+        with np.load(path) as z:
+            res[name] = {k: z[k] for k in z.files}
+    assert any(k.startswith("irl_kernel<5,7,1,112,4,2>") for k in res["default"]["kernels"]), res["default"]["kernels"]
+    assert not any(k.startswith("irl_kernel<5,7,1,112,4,2>") for k in res["no_irl2"]["kernels"])
+    for k in res["default"]:
+        if k != "kernels":
+            assert np.array_equal(res["default"][k], res["no_irl2"][k]), (k, float(np.abs(res["default"][k] - res["no_irl2"][k]).max()))

@@ -45,36 +45,45 @@ constexpr int IRL_CEC = 16;  // expanded channels per chunk
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // HW: input plane side; S: the depthwise stride (TF-style 'same' padding: the output plane is
-// HW / S); CX: block-input channels (the expand's K); MP: 32-row slices of the projection (Mpad / 32)
-template <int K, int HW, int S, int CX, int MP>
+// HW / S); CX: block-input channels (the expand's K); MP: 32-row slices of the projection (Mpad / 32);
+// NI: images per workgroup (2 at 7^2: each M wave then runs two independent MFMA chains, and a
+// few hundred ROIs fill the CUs in one round instead of one and a third)
+template <int K, int HW, int S, int CX, int MP, int NI>
 __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPwParams D) {
     constexpr int HO = HW / S, P = HW * HW, PO = HO * HO, PL = S == 1 ? K / 2 : K / 2 - 1;
     constexpr int PH = (HO - 1) * S + K, PW = (PH + 1) & ~1, PP = PH * PW;  // padded plane (even rows)
-    constexpr int NE = (P + 15) / 16, NEW = (NE + 3) / 4;                    // expand column tiles (per M wave)
-    constexpr int NCT = (PO + 31) / 32, NCP = NCT * 32;                     // projection column tiles
-    constexpr int CPW = 4 / MP, TPW = (NCT + CPW - 1) / CPW;           // tile stride, tiles per M wave
+    constexpr int NE = (P + 15) / 16, NET = NI * NE, NEW = (NET + 3) / 4;   // expand column tiles (per M wave)
+    constexpr int NCT = (PO + 31) / 32, NCP = NCT * 32, NCTT = NI * NCT;    // projection column tiles (per image)
+    constexpr int CPW = 4 / MP, TPW = (NCTT + CPW - 1) / CPW;          // tile stride, tiles per M wave
     constexpr int KS = CX / 4, KK = K * K, NSW = IRL_CEC * KK + IRL_CEC;
     // depthwise task: RW outputs of a row (a half row when whole rows leave half the D threads idle)
     constexpr int RW = IRL_CEC * HO * 2 <= 256 && HO % 2 == 0 ? HO / 2 : HO, RPR = HO / RW;
     constexpr int WWIN = ((RW - 1) * S + K + 1) & ~1;  // window floats per input row (even)
     constexpr bool W64 = RW == HO || S == 2;           // 8-byte aligned window starts: 8-byte reads
-    static_assert(4 % MP == 0 && CX % 4 == 0 && IRL_CEC * HO * RPR <= 256 && NE >= 4 && HW % S == 0, "irl layout");
-    __shared__ __attribute__((aligned(16))) float sE[2][IRL_CEC * PP];  // expanded planes (zero border)
-    __shared__ __attribute__((aligned(16))) float sD[2][IRL_CEC * NCP];  // depthwise tiles
+    constexpr int NTASK = IRL_CEC * HO * RPR;          // depthwise tasks per image
+    static_assert(4 % MP == 0 && CX % 4 == 0 && NI * NTASK <= 256 && NE >= 4 && HW % S == 0, "irl layout");
+    // image j of the workgroup: planes sE[.][j][c], tile columns sD[.][c][j * NCP + q]
+    __shared__ __attribute__((aligned(16))) float sE[2][NI * IRL_CEC * PP];  // expanded planes (zero border)
+    __shared__ __attribute__((aligned(16))) float sD[2][IRL_CEC * NI * NCP];  // depthwise tiles
     __shared__ float sW[2][NSW];  // a chunk's depthwise weights, then its biases
+    // the M waves' operands of step t in sM[t & 1]: chunk t's expand weights [CX][16] and biases,
+    // then chunk t - 2's projection weights [16][MP * 32]
+    constexpr int MWA = 0, MB = CX * IRL_CEC, MW2 = MB + IRL_CEC, NSM = MW2 + IRL_CEC * MP * 32;
+    __shared__ __attribute__((aligned(16))) float sM[2][NSM];
 
     const GemmParams &G = D.g;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int n = blockIdx.x;
-    if (G.nact && n >= *G.nact) return;  // (whole workgroup, before any barrier)
+    const int n0 = blockIdx.x * NI;  // images n0 .. n0 + NI - 1 below nlim
+    const int nimg = D.g.ncols / PO, nlim = G.nact && *G.nact < nimg ? *G.nact : nimg;
+    if (n0 >= nlim) return;  // (whole workgroup, before any barrier)
     const int nch = E.M / IRL_CEC;
     const bool mrole = wave < 4;         // waves 0-3: MFMA (expand, projection); 4-7: depthwise
 
-    for (int i = tid; i < 2 * IRL_CEC * PP; i += 512) (&sE[0][0])[i] = 0.f;  // the borders stay 0
+    for (int i = tid; i < 2 * NI * IRL_CEC * PP; i += 512) (&sE[0][0])[i] = 0.f;  // the borders stay 0
 
     // ---- M waves: expand operands (lane (col, kq): x[4 s + kq][t * 16 + col] of tiles
-    // t = wave + 4 i as B; W1[c0 + col][4 s + kq] as A) and projection accumulators (32-row slice
-    // m0, column tiles ct0, ct0 + CPW, ...)
+    // t = wave + 4 i as B -- tile t is tile t % NE of image t / NE; W1[c0 + col][4 s + kq] as A)
+    // and projection accumulators (32-row slice m0, column tiles ct0, ct0 + CPW, ...)
     const int col = lane & 15, kq = lane >> 4;
     const int mw = wave & 3;
     const int m0 = (mw % MP) * 32, ct0 = mw / MP;
@@ -82,11 +91,12 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
     float xr[NEW][KS];
     f32x16 acc[TPW];
     if (mrole) {
-        const float *xb = E.x + (size_t)(uint32_t)n * (uint32_t)E.x_sN;
 #pragma unroll
         for (int i = 0; i < NEW; ++i) {
-            const int p = (mw + 4 * i) * 16 + col;
-            const uint32_t pc = p < P ? (uint32_t)p : 0u;
+            const int t = mw + 4 * i, j = t / NE, p = (t - j * NE) * 16 + col;
+            const int ni = t < NET && n0 + j < nlim ? n0 + j : n0;
+            const float *xb = E.x + (size_t)(uint32_t)ni * (uint32_t)E.x_sN;
+            const uint32_t pc = t < NET && p < P ? (uint32_t)p : 0u;
 #pragma unroll
             for (int s = 0; s < KS; ++s) xr[i][s] = xb[(uint32_t)(4 * s + kq) * (uint32_t)E.x_sC + pc];
         }
@@ -97,33 +107,44 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
     }
     const Bounds eb = bounds(E.pre), db = bounds(D.dw_act);  // (E.post: none, host-checked)
 
-    // M-wave operands, two steps ahead: set t & 1 holds the expand's A operands and biases of
-    // chunk t and the projection's A operands of chunk t - 2; each part is reloaded (for step t + 2)
-    // right after its last use in step t, into the same registers (a copy would wait for the
-    // loads), with chunk indices clamped past the ends
-    struct Ops {
-        float wa[KS], bias[4], w2[IRL_CEC / 2];
-    };
-    auto load_e = [&](int ce, Ops &o) {
-        const int c0 = (ce < nch ? ce : nch - 1) * IRL_CEC;
-#pragma unroll
-        for (int s = 0; s < KS; ++s) o.wa[s] = E.wt[(uint32_t)(4 * s + kq) * (uint32_t)E.Mpad + (uint32_t)(c0 + col)];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o.bias[r] = E.bias[c0 + 4 * kq + r];
-    };
-    auto load_p = [&](int cp, Ops &o) {
-        const int c2 = (cp < 0 ? 0 : cp < nch ? cp : nch - 1) * IRL_CEC;
-#pragma unroll
-        for (int s = 0; s < IRL_CEC / 2; ++s)
-            o.w2[s] = G.wt[(uint32_t)(c2 + 2 * s + kh) * (uint32_t)G.Mpad + (uint32_t)(m0 + pcol)];
-    };
-
     // ---- D waves: channel dc of a chunk, outputs dx0 .. dx0 + RW - 1 of row dy
     const int dt = tid - 256;
-    const bool dw_on = !mrole && dt < IRL_CEC * HO * RPR;
-    const int dc = dw_on ? dt / (HO * RPR) : 0, dr = dt - dc * HO * RPR, dy = dr / RPR, dx0 = (dr - dy * RPR) * RW;
-    // chunk c's depthwise weights and biases: loaded a step ahead into registers (NSW <= 512:
-    // two words per D thread), stored to LDS in the step before their use
+    const bool dw_on = !mrole && dt < NI * NTASK;
+    const int dj = dw_on ? dt / NTASK : 0, dtj = dt - dj * NTASK;  // image dj of the workgroup
+    const int dc = dw_on ? dtj / (HO * RPR) : 0, dr = dtj - dc * HO * RPR, dy = dr / RPR, dx0 = (dr - dy * RPR) * RW;
+    // The D waves stage every weight through LDS, loaded a step ahead into registers and stored
+    // in the step before their use; the M waves then issue no memory loads in the step loop
+    // (the compiler's vmcnt waits for operand registers loaded one or two steps earlier counted
+    // the newest loads too, so each step paid a whole memory latency).
+    // M operands of step ce: 16-byte pieces (expand rows of 16, biases, projection rows),
+    // chunk indices clamped past the ends.
+    constexpr int NF = NSM / 4, NFR = (NF + 255) / 256;
+    float mr[4 * NFR];  // (scalars: a float4 array of this shape was kept in scratch)
+    auto load_m = [&](int ce) {
+        const int c0 = (ce < nch ? ce : nch - 1) * IRL_CEC;
+        const int c2 = (ce < 2 ? 0 : ce - 2 < nch ? ce - 2 : nch - 1) * IRL_CEC;
+#pragma unroll
+        for (int j = 0; j < NFR; ++j) {
+            // (branch-free, from a clamped piece: a private array behind branches goes to scratch)
+            const int f = dt + 256 * j < NF ? dt + 256 * j : NF - 1, e = 4 * f;
+            const int k = e / IRL_CEC, r = (e - MW2) / (MP * 32);
+            const uint32_t oa = (uint32_t)k * (uint32_t)E.Mpad + (uint32_t)(c0 + e - k * IRL_CEC);
+            const uint32_t ob = (uint32_t)(c0 + e - MB);
+            const uint32_t o2 = (uint32_t)(c2 + r) * (uint32_t)G.Mpad + (uint32_t)(e - MW2 - r * MP * 32);
+            const float *src = e < MB ? E.wt + oa : e < MW2 ? E.bias + ob : G.wt + o2;
+            const float4 v = *reinterpret_cast<const float4 *>(src);
+            mr[4 * j] = v.x;
+            mr[4 * j + 1] = v.y;
+            mr[4 * j + 2] = v.z;
+            mr[4 * j + 3] = v.w;
+        }
+    };
+    auto store_m = [&](int ce) {
+#pragma unroll
+        for (int j = 0; j < NFR; ++j)
+            if (dt + 256 * j < NF) reinterpret_cast<float4 *>(sM[ce & 1])[dt + 256 * j] = make_float4(mr[4 * j], mr[4 * j + 1], mr[4 * j + 2], mr[4 * j + 3]);
+    };
+    // chunk c's depthwise weights and biases (NSW <= 512: two words per D thread)
     constexpr int NSR = (NSW + 255) / 256;
     float swr[NSR];
     auto load_w = [&](int c) {
@@ -138,61 +159,70 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
     // Step t: the M waves expand chunk t into sE[t & 1] and project chunk t - 2 from sD[t & 1];
     // the D waves run chunk t - 1's depthwise (sE[(t - 1) & 1] -> sD[(t - 1) & 1]) and stage chunk
     // t's depthwise weights.  One barrier per step hands the buffers over.
-    auto step = [&](int t, Ops &o) {
+    auto step = [&](int t) {
+        const float *sm = sM[t & 1];
         if (mrole) {
             if (t < nch) {
                 // expand; each tile's MFMA chain is issued before the previous tile's epilogue
                 float *pe = sE[t & 1];
+                float wa[KS], bias[4];
+#pragma unroll
+                for (int s = 0; s < KS; ++s) wa[s] = sm[MWA + (4 * s + kq) * IRL_CEC + col];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) bias[r] = sm[MB + 4 * kq + r];
                 auto chain = [&](int i) {
                     f32x4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                    for (int s = 0; s < KS; ++s) d = __builtin_amdgcn_mfma_f32_16x16x4f32(o.wa[s], xr[i][s], d, 0, 0, 0);
+                    for (int s = 0; s < KS; ++s) d = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[s], xr[i][s], d, 0, 0, 0);
                     return d;
                 };
                 auto epi = [&](int i, const f32x4 &d) {  // gemm_tiled_kernel's epilogue (RES = false)
-                    const int p = (mw + 4 * i) * 16 + col;
+                    const int t = mw + 4 * i, j = t / NE, p = (t - j * NE) * 16 + col;
                     if (p < P) {
                         const int y = p / HW, x = p - y * HW;
-                        float *e = pe + (4 * kq) * PP + (y + PL) * PW + x + PL;
+                        float *e = pe + (j * IRL_CEC + 4 * kq) * PP + (y + PL) * PW + x + PL;
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) e[r * PP] = clamp(eb, d[r] + o.bias[r]);
+                        for (int r = 0; r < 4; ++r) e[r * PP] = clamp(eb, d[r] + bias[r]);
                     }
                 };
                 f32x4 dcur = chain(0);
 #pragma unroll
                 for (int i = 0; i < NEW; ++i) {
                     f32x4 dn = dcur;
-                    if (i + 1 < NEW && mw + 4 * (i + 1) < NE) dn = chain(i + 1);
-                    if (mw + 4 * i < NE) epi(i, dcur);  // (wave-uniform)
+                    if (i + 1 < NEW && mw + 4 * (i + 1) < NET) dn = chain(i + 1);
+                    if (mw + 4 * i < NET) epi(i, dcur);  // (wave-uniform)
                     dcur = dn;
                 }
-                load_e(t + 2, o);
             }
             if (t >= 2) {
                 // projection: acc += W2[m0 .. m0 + 31][chunk t - 2] x its depthwise tile
                 const float *pd = sD[t & 1];
 #pragma unroll
                 for (int s = 0; s < IRL_CEC / 2; ++s) {
-                    const float *b = pd + (2 * s + kh) * NCP + pcol;
+                    const float w2 = sm[MW2 + (2 * s + kh) * (MP * 32) + m0 + pcol];
+                    const float *b = pd + (2 * s + kh) * (NI * NCP) + pcol;
 #pragma unroll
                     for (int i = 0; i < TPW; ++i) {
                         const int ct = ct0 + CPW * i;
-                        if (ct < NCT) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(o.w2[s], b[ct * 32], acc[i], 0, 0, 0);
+                        if (ct < NCTT) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(w2, b[ct * 32], acc[i], 0, 0, 0);
                     }
                 }
-                load_p(t, o);
             }
         } else {
+            // the stores of last step's loads first: a store after this step's loads would wait
+            // for them too
             if (t < nch) {
 #pragma unroll
                 for (int j = 0; j < NSR; ++j)
                     if (dt + 256 * j < NSW) sW[t & 1][dt + 256 * j] = swr[j];
-                load_w(t + 1);
             }
+            store_m(t + 1);  // (read in step t + 1; step t reads the other buffer)
+            if (t < nch) load_w(t + 1);
+            load_m(t + 2);
             if (t >= 1 && t <= nch && dw_on) {
                 // depthwise of chunk t - 1: RW outputs of one row of one channel, each input row once
                 const float *w = sW[(t - 1) & 1] + dc * KK;
-                const float *pe = sE[(t - 1) & 1] + dc * PP + dx0 * S;
+                const float *pe = sE[(t - 1) & 1] + (dj * IRL_CEC + dc) * PP + dx0 * S;
                 float a[RW];
                 const float bb = sW[(t - 1) & 1][IRL_CEC * KK + dc];
 #pragma unroll
@@ -219,7 +249,7 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
                         for (int o = 0; o < RW; ++o) a[o] = __builtin_fmaf(wt, xw[o * S + kx], a[o]);
                     }
                 }
-                float *dst = sD[(t - 1) & 1] + dc * NCP + dy * HO + dx0;
+                float *dst = sD[(t - 1) & 1] + dc * (NI * NCP) + dj * NCP + dy * HO + dx0;
 #pragma unroll
                 for (int o = 0; o < RW; ++o) dst[o] = clamp(db, a[o]);
             }
@@ -227,42 +257,51 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
         lds_barrier();
     };
 
-    Ops S0, S1;
-    if (mrole) {
-        load_e(0, S0);
-        load_p(0, S0);
-        load_e(1, S1);
-        load_p(1, S1);
-    } else {
+    if (!mrole) {
         load_w(0);
+        load_m(0);
+        store_m(0);
+        load_m(1);
     }
-    lds_barrier();  // the zeroed planes
-    for (int t = 0; t < nch + 2; t += 2) {  // (nch even, host-checked: set t & 1 is static)
-        step(t, S0);
-        step(t + 1, S1);
+    lds_barrier();  // the zeroed planes, step 0's M operands
+    for (int t = 0; t < nch + 2; t += 2) {  // (nch even, host-checked: buffer t & 1 is static)
+        step(t);
+        step(t + 1);
     }
 
     if (mrole) {
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
-            const int ct = ct0 + CPW * i;
-            const int q = ct * 32 + pcol;
-            if (ct < NCT && q < PO) {
+            const int ct = ct0 + CPW * i, j = ct / NCT;
+            const int q = (ct - j * NCT) * 32 + pcol;
+            if (ct < NCTT && q < PO && n0 + j < nlim) {
                 // opaque row base / half: otherwise the compiler hoists every row's channel index
                 // and bias / residual address out of the step loop and holds them across it
                 int mb = m0, h = kh;
                 asm volatile("" : "+v"(mb), "+v"(h));
-                epilogue_tile(G, acc[i], n, q, mb, h);
+                epilogue_tile(G, acc[i], n0 + j, q, mb, h);
             }
         }
     }
 }
 
-template <int K, int HW, int S, int CX, int MP>
+template <int K, int HW, int S, int CX, int MP, int NI = 1>
 const char *irl_go(const GemmParams &e, const DwPwParams &d, hipStream_t s) {
     const int N = d.g.ncols / ((HW / S) * (HW / S));
-    hipLaunchKernelGGL((irl_kernel<K, HW, S, CX, MP>), dim3(N), dim3(512), 0, s, e, d);
-    return kernel_name("irl_kernel<%d,%d,%d,%d,%d>", K, HW, S, CX, MP);
+    hipLaunchKernelGGL((irl_kernel<K, HW, S, CX, MP, NI>), dim3((N + NI - 1) / NI), dim3(512), 0, s, e, d);
+    return NI == 1 ? kernel_name("irl_kernel<%d,%d,%d,%d,%d>", K, HW, S, CX, MP)
+                   : kernel_name("irl_kernel<%d,%d,%d,%d,%d,%d>", K, HW, S, CX, MP, NI);
+}
+
+// CUs of the current device
+int cu_count() {
+    static const int ncu = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return n;
+    }();
+    return ncu;
 }
 
 }  // namespace
@@ -282,11 +321,18 @@ const char *launch_irl(const GemmParams &e, const DwPwParams &d, hipStream_t s) 
         e.M % (2 * IRL_CEC) != 0 || e.post.kind != ACT_NONE || !bounds_act(e.pre) || !bounds_act(d.dw_act))
         return nullptr;
     const int hw = d.in.W, cx = e.K, mp = d.g.Mpad / 32;
-    if (d.g.Mpad % 32 != 0) return nullptr;
+    // (the weights are staged in 16-byte pieces)
+    if (d.g.Mpad % 32 != 0 || e.Mpad % 4 != 0 || ((uintptr_t)e.wt | (uintptr_t)e.bias | (uintptr_t)d.g.wt) % 16 != 0)
+        return nullptr;
     if (S == 1 && d.k == 3 && hw == 14 && cx == 48 && mp == 2) return irl_go<3, 14, 1, 48, 2>(e, d, s);
     if (S == 1 && d.k == 5 && hw == 14 && cx == 48 && mp == 2) return irl_go<5, 14, 1, 48, 2>(e, d, s);
     if (S == 1 && d.k == 5 && hw == 14 && cx == 64 && mp == 2) return irl_go<5, 14, 1, 64, 2>(e, d, s);
-    if (S == 1 && d.k == 5 && hw == 7 && cx == 112 && mp == 4) return irl_go<5, 7, 1, 112, 4>(e, d, s);
+    if (S == 1 && d.k == 5 && hw == 7 && cx == 112 && mp == 4) {
+        // two images per workgroup once the images outnumber the CUs (below that, halving the
+        // workgroups leaves CUs idle)
+        if (form_on(FORM_IRL2) && d.g.ncols / d.g.P > cu_count()) return irl_go<5, 7, 1, 112, 4, 2>(e, d, s);
+        return irl_go<5, 7, 1, 112, 4>(e, d, s);
+    }
     if (S == 2 && d.k == 5 && hw == 14 && cx == 64 && mp == 4) return irl_go<5, 14, 2, 64, 4>(e, d, s);
     return nullptr;
 }
