@@ -333,7 +333,10 @@ const char *launch_irl(const GemmParams &e, const DwPwParams &d, hipStream_t s) 
         if (form_on(FORM_IRL2) && d.g.ncols / d.g.P > cu_count()) return irl_go<5, 7, 1, 112, 4, 2>(e, d, s);
         return irl_go<5, 7, 1, 112, 4>(e, d, s);
     }
-    if (S == 2 && d.k == 5 && hw == 14 && cx == 64 && mp == 4) return irl_go<5, 14, 2, 64, 4>(e, d, s);
+    if (S == 2 && d.k == 5 && hw == 14 && cx == 64 && mp == 4) {
+        if (form_on(FORM_IRL2) && d.g.ncols / d.g.P > cu_count()) return irl_go<5, 14, 2, 64, 4, 2>(e, d, s);
+        return irl_go<5, 14, 2, 64, 4>(e, d, s);
+    }
     return nullptr;
 }
 
