@@ -130,15 +130,22 @@ __global__ __launch_bounds__(256) void ir_kernel(const GemmParams E, const DwPwP
     }
 
     const Bounds eb = bounds(E.pre), db = bounds(D.dw_act);  // (E.post: none, host-checked)
+    // expand operands of a chunk: A[m][k] = W1[c0 + m][k] from the transposed [Kpad][Mpad]
+    // weights, and the biases (c0 < Ce: host-checked Ce % 16 == 0; clamped past the end).  Loaded
+    // a chunk ahead: loaded in the chunk that uses them, every chunk waited a memory latency.
+    auto load_ab = [&](int c0, float (&aa)[4], float (&bb)[4]) {
+        c0 = c0 < Ce ? c0 : Ce - IR_CEC;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) aa[s] = E.wt[(uint32_t)(4 * s + kq) * (uint32_t)E.Mpad + (uint32_t)(c0 + col)];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bb[r] = E.bias[c0 + 4 * kq + r];
+    };
+    float a[4], bias[4];
+    load_ab(0, a, bias);
     for (int c0 = 0; c0 < Ce; c0 += IR_CEC) {
-        // 1. expand: A[m][k] = W1[c0 + m][k] from the transposed [Kpad][Mpad] weights (rows past Ce: 0)
-        const int cm = c0 + col;
-        float a[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) a[s] = E.wt[(uint32_t)(4 * s + kq) * (uint32_t)E.Mpad + (uint32_t)cm];
-        float bias[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bias[r] = E.bias[c0 + 4 * kq + r];  // (< Ce: host-checked Ce % 16 == 0)
+        // 1. expand
+        float an[4], bn[4];
+        load_ab(c0 + IR_CEC, an, bn);
         // each column tile's MFMA chain is issued before the previous tile's epilogue, so the
         // epilogue's VALU work covers the chain's latency
         auto chain = [&](int i) {
@@ -193,6 +200,11 @@ __global__ __launch_bounds__(256) void ir_kernel(const GemmParams E, const DwPwP
             }
         }
         __syncthreads();  // the chunk's readers are done
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            a[s] = an[s];
+            bias[s] = bn[s];
+        }
     }
 
     if (!active) return;
