@@ -93,7 +93,11 @@ def sub_batches(args, kind):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); N > 1 without WORLD_SIZE set: this process starts the N ranks "
+                         "itself (zaru_amd/launch.py), under torchrun WORLD_SIZE must equal N")
+    ap.add_argument("--rank-timeout", type=float, default=1500.0,
+                    help="launcher only: seconds before the N ranks are stopped and the run fails")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1024, help="frames per step per GPU")
@@ -431,9 +435,19 @@ def run_steps(workloads, steps, gather, rank, world, pool):
 
 def main():
     args = parse()
+    from zaru_amd import launch
+    try:
+        world = launch.world_from_env(args.gpus)
+    except ValueError as e:
+        print(f"bench.py: {e}", file=sys.stderr)
+        sys.exit(2)
+    if world is None:
+        # --gpus N > 1 without an outside launcher: start the N ranks here (child processes,
+        # before this process touches the GPU) and exit with their verdict
+        sys.exit(launch.run_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                  args.gpus, args.rank_timeout))
     Workload.device_post = not args.host_post
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     primary = args.workload if args.workload in ("hand", "face_next") else "face"
     # child processes first, while this one has not touched the GPU: PMC traffic passes,
@@ -524,6 +538,10 @@ def main():
         g = wls[0].pipe.gathered()
         ids = np.sort(g[:, 0].view(np.uint32))
         gather_check = bool(np.array_equal(ids, np.arange(world * args.batch, dtype=np.uint32)))
+    elif gather is not None:  # the shared-GPU dry run: the gloo gather of the last step
+        g = gather.result(gather.steps - 1).numpy()
+        ids = np.sort(g[:, 0].view(np.uint32))
+        gather_check = bool(np.array_equal(ids, np.arange(world * args.batch * len(wls), dtype=np.uint32)))
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)  # gloo control group: host tensors
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -587,6 +605,9 @@ def main():
                             "one-rank communicator)" if comms else ""))},
         "prime": primed,
         "gather_check": gather_check,
+        "rccl_ranks": comms[0].size() if comms else None,
+        "launcher": ("bench.py --gpus" if os.environ.get("ZARU_BENCH_LAUNCHED") == "1" else "external")
+                    if world > 1 else None,
         "frames_per_s": round(frames / elapsed, 1),
         "rois_per_s": round(rois / elapsed, 1),
         "tracked_per_step": round(tracked / args.steps / world, 2),
@@ -627,6 +648,7 @@ def main():
         out["face_next"] = next_line(H, args, device, side_traffic.get("face_next"))
     if world == 1 and args.workload == "face" and not args.no_tracking:
         out["tracking"] = tracking_line(H, args, device, wl)
+        out["face_loop"] = face_loop_line(H, args, device, wl)
         out["hand_tracking"] = hand_tracking_line(H, args, device, wl)
     if world == 1 and args.workload == "face" and not args.no_c5:
         out["config5"] = c5_line(H, args, device, wl)
@@ -710,6 +732,57 @@ def tracking_line(H, args, device, wl):
             "pipeline_roofline": {"model": "SURVEY.md §8d FaceMesh bytes + 192^2 preprocessing per face",
                                   "bytes_per_face": round(bpf), "achieved_GBs": round(fps * bpf / 1e9, 1),
                                   "frac": round(fps * bpf / 1e9 / HBM_PEAK_GBS, 4)}}
+
+
+def face_loop_line(H, args, device, wl, streams=256, sets=8):
+    """The reference demo's face video loop (examples/facemesh.rs:35-56: BlazeFace short range +
+    FaceMesh V2, track and detect only when tracking is lost, re-seed from the most confident
+    face) with its state on the device (DeviceFaceLoop).  `streams` camera streams
+    over a `sets`-frame synthetic video of 1080p frames, cycled: each stream's face patch drifts
+    4/6 px per frame, and on every other stream the face leaves one frame of the cycle (a
+    different frame per stream), so the tracker loses it, the detector runs on that frame (no
+    face) and the next one (face found: re-seeded), and tracking resumes on the frame after.
+    No host decision between frames.  value = tracked faces (FaceMesh results) per second."""
+    import torch
+    fs = wl.fs
+    dev = f"cuda:{device}"
+    patch = torch.from_numpy(load_patch()).to(dev)
+    base = torch.from_numpy(fs.base).to(dev)
+    ph, pw = patch.shape[:2]
+    video = torch.empty((sets, streams, fs.h, fs.w, 4), dtype=torch.uint8, device=dev)
+    hidden = 0
+    for v in range(sets):
+        for s in range(streams):
+            video[v, s].copy_(base[s % len(fs.base)])
+            if s % 2 == 0 and (s // 2) % sets == v:
+                hidden += 1
+                continue
+            y, x = fs.pos[s]
+            y, x = min(fs.h - ph, y + 4 * v), min(fs.w - pw, x + 6 * v)
+            video[v, s, y:y + ph, x:x + pw] = patch
+    torch.cuda.synchronize(device)
+    lists = [[(video[v, s].data_ptr(), fs.w, fs.h, fs.w * 4) for s in range(streams)] for v in range(sets)]
+    loop = H.DeviceFaceLoop("face", "facemesh_v2", streams, device)
+    for k in range(2 * sets):  # first frame: every stream detects (no RoI yet), then the cycle
+        loop.step(lists[k % sets])
+    loop.synchronize()
+    d0, r0 = loop.detections_run(), loop.reacquisitions()
+    steps = max(sets, args.tracking_steps // sets * sets)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        loop.step(lists[k % sets])
+    loop.synchronize()
+    elapsed = time.perf_counter() - t0
+    dets, reacq = loop.detections_run() - d0, loop.reacquisitions() - r0
+    tracked = streams * steps - dets  # a stream detects exactly when its track() returned None
+    del loop, video
+    return {"metric": "tracked faces/sec, the face demo's video loop on the device (examples/facemesh.rs:35-56: "
+                      "FaceMesh V2 tracking, BlazeFace short range only on lost streams, re-seed from the best face)",
+            "value": round(tracked / elapsed, 1), "unit": "faces/s", "streams": streams, "steps": steps,
+            "ms_per_step": round(1e3 * elapsed / steps, 3),
+            "video": f"{sets}-frame 1080p cycle; {hidden} of {streams * sets} stream-frames without the face",
+            "detections_run": int(dets), "reacquisitions": int(reacq),
+            "tracked_results": int(tracked)}
 
 
 def hand_tracking_line(H, args, device, wl, streams=256, slots=4):

@@ -265,6 +265,23 @@ int zr_cnn_estimate_device_views_count_async(zr_session *s, const zr_frame *fram
  * d_total (may be NULL): *d_total += *d_ndue, a running count of the detections run. */
 int zr_due_compact_async(const int32_t *d_det_pending, size_t n, const zr_view_desc *view_template, int32_t *d_due,
                          int32_t *d_ndue, zr_view_desc *d_due_views, uint64_t *d_total, void *hip_stream);
+/* The face video loop of the reference's demo (crates/zaru/examples/facemesh.rs:35-56: track, and
+ * on loss detect on the same frame and re-seed the tracker from the most confident detection) on
+ * the device, in two calls around a mapped detection (zr_cnn_estimate_device_views_count_async +
+ * zr_detect_post_mapped_async).  zr_track_lost_compact_async: as zr_due_compact_async, with the
+ * streams whose state holds no RoI (active == 0: lost by this step's zr_track_update_async or
+ * never seeded, LandmarkTracker::roi() == None) as the due streams.  zr_track_reseed_best_async:
+ * every stream without RoI whose detection found a face (d_count / d_dets as the mapped
+ * post-processing wrote its slot) gets RoI = RotatedRect(best.rect, 0) for best =
+ * max_by_key(TotalF32(confidence)) (the last of equal maxima; LandmarkTracker::set_roi,
+ * landmark.rs:434-436), active = 1, and its next view in d_views; other streams are untouched.
+ * d_reseeded (may be NULL): += the streams re-seeded. */
+int zr_track_lost_compact_async(const zr_track_state *d_state, size_t n, const zr_view_desc *view_template,
+                                int32_t *d_due, int32_t *d_ndue, zr_view_desc *d_due_views, uint64_t *d_total,
+                                void *hip_stream);
+int zr_track_reseed_best_async(const int32_t *d_count, const float *d_dets, size_t dcap, const uint32_t *d_frame_size,
+                               size_t n, const zr_track_cfg *cfg, zr_track_state *d_state, zr_view_desc *d_views,
+                               uint64_t *d_reseeded, void *hip_stream);
 
 /* ---- JPEG frame source --------------------------------------------------
  * Replaces decode_jpeg (crates/zaru-image/src/jpeg.rs:107-182) for its libjpeg-turbo backend

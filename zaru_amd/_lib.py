@@ -56,6 +56,8 @@ SIGNATURES = [
     ("zr_detect_post_async", _I, [_P, _P, _P, _P, _SZ, _P, _P, _P, _SZ, _P, _SZ, _U32, _U32, _P, _P]),
     ("zr_detect_post_mapped_async", _I, [_P, _P, _P, _P, _SZ, _P, _P, _P, _P, _P, _SZ, _P, _P]),
     ("zr_due_compact_async", _I, [_P, _SZ, _P, _P, _P, _P, _P, _P]),
+    ("zr_track_lost_compact_async", _I, [_P, _SZ, _P, _P, _P, _P, _P, _P]),
+    ("zr_track_reseed_best_async", _I, [_P, _P, _SZ, _P, _SZ, _P, _P, _P, _P, _P]),
     ("zr_cnn_estimate_device_views_count_async", _I, [_P, _P, _SZ, _P, _SZ, _P, _F, _F, _P, _P]),
     ("zr_track_seed_detections_async", _I, [_P, _P, _SZ, _P, _P, _P, _SZ, _P, _F, _I, _P, _P, _P, _P]),
     ("zr_hand_manage_async", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P, _SZ, _P, C.c_double, _I,

@@ -10,6 +10,7 @@
 #include "device_hand_tracker.h"
 #include "landmark.h"
 #include "pipeline.h"
+#include "device_face_loop.h"
 #include "device_tracker.h"
 
 namespace py = pybind11;
@@ -410,6 +411,58 @@ PYBIND11_MODULE(_zaru_host, m) {
             std::memcpy(a.mutable_data(), v.data(), v.size() * 4);
             return a;
         });
+
+    // examples/facemesh.rs:35-56 on the device: track, detect on loss, re-seed from the best face
+    py::class_<DeviceFaceLoop>(m, "DeviceFaceLoop")
+        .def(py::init([](const std::string &detector, const std::string &landmarker, size_t streams, int device,
+                         float padding, float loss, float det_threshold) {
+                 return new DeviceFaceLoop(detector_net(detector), landmark_net(landmarker), streams, device, padding,
+                                           loss, det_threshold);
+             }), py::arg("detector") = "face", py::arg("landmarker") = "facemesh_v2", py::arg("streams") = 1,
+             py::arg("device") = 0, py::arg("padding") = LandmarkTracker::DEFAULT_ROI_PADDING,
+             py::arg("loss_threshold") = LandmarkTracker::DEFAULT_LOSS_THRESHOLD,
+             py::arg("det_threshold") = Detector::DEFAULT_THRESHOLD)
+        .def("set_roi", &DeviceFaceLoop::set_roi)
+        .def("step", [](DeviceFaceLoop &t, const std::vector<std::tuple<uint64_t, uint32_t, uint32_t, uint64_t>> &frames) {
+            std::vector<Image> im;
+            for (auto &f : frames) {
+                Image i;
+                i.rgba = reinterpret_cast<const uint8_t *>(std::get<0>(f));
+                i.width = std::get<1>(f);
+                i.height = std::get<2>(f);
+                i.row_stride = std::get<3>(f);
+                i.on_device = true;
+                im.push_back(i);
+            }
+            py::gil_scoped_release nogil;
+            t.step(im);
+        })
+        .def("synchronize", &DeviceFaceLoop::synchronize, py::call_guard<py::gil_scoped_release>())
+        .def("__len__", &DeviceFaceLoop::streams)
+        .def("states", [](DeviceFaceLoop &t) {
+            py::list out;
+            for (const auto &s : t.states()) {
+                py::dict d;
+                d["roi"] = RotatedRect(Rect::from_center(s.roi[0], s.roi[1], s.roi[2], s.roi[3]), s.roi[4]);
+                d["updated_roi"] = RotatedRect(Rect::from_center(s.updated[0], s.updated[1], s.updated[2], s.updated[3]), s.updated[4]);
+                d["view_rect"] = RotatedRect(Rect::from_center(s.view_rect[0], s.view_rect[1], s.view_rect[2], s.view_rect[3]), s.view_rect[4]);
+                d["active"] = s.active != 0;
+                d["tracked"] = s.tracked != 0;
+                d["confidence"] = s.confidence;
+                out.append(d);
+            }
+            return out;
+        })
+        .def("landmarks", [](DeviceFaceLoop &t) {
+            auto v = t.landmarks();
+            py::array_t<float> a({(py::ssize_t)t.streams(), (py::ssize_t)t.landmarker().num_landmarks, (py::ssize_t)3});
+            std::memcpy(a.mutable_data(), v.data(), v.size() * 4);
+            return a;
+        })
+        .def("detected", &DeviceFaceLoop::detected)
+        .def("detection_counts", &DeviceFaceLoop::detection_counts)
+        .def("detections_run", &DeviceFaceLoop::detections_run)
+        .def("reacquisitions", &DeviceFaceLoop::reacquisitions);
 
     py::class_<DetectTrackPipeline>(m, "DetectTrackPipeline")
         .def(py::init([](const std::string &kind, int device, int threads, uint32_t max_rois,

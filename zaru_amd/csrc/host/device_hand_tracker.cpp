@@ -125,6 +125,13 @@ void DeviceHandTracker::step(const std::vector<Image> &frames, double now_ms) {
         check(zr_stream_synchronize(stream_));
         const zr_view pv = to_zr_view(letterbox_view(W, H, palm_->aspect()));
         check(zr_view_describe(&pv, 1, 0, &palm_tmpl_));
+        // every entry of the due-view table holds a valid view from the start (stream i's
+        // letterbox): due_compact writes only the first ndue, and a palm preprocessing that does
+        // not honour the device count (an unfused plan) samples all n_ entries
+        std::vector<zr_view_desc> dv(n_, palm_tmpl_);
+        for (size_t i = 0; i < n_; i++) dv[i].frame = (uint32_t)i;
+        check(zr_memcpy_async(due_views_.ptr, dv.data(), n_ * sizeof(zr_view_desc), 0, stream_));
+        check(zr_stream_synchronize(stream_));
     }
     // injected detections replace the palm result this step consumes (test hook)
     bool any = false;

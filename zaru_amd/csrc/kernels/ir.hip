@@ -271,7 +271,10 @@ const char *launch_ir(const GemmParams &e, const DwPwParams &d, hipStream_t s) {
     if (d.g.res_mode != 0 && (d.g.r != e.x || d.g.r_C > IR_CX || d.g.r_sC != e.x_sC || d.g.r_sN != e.x_sN))
         return nullptr;
     if (d.g.res_mode == 1 && d.stride != 1) return nullptr;
-    if (d.g.res_mode == 2 && (d.stride != 2 || d.g.r_W != d.in.W)) return nullptr;
+    // the max-pool shortcut is read at footprint (2ty, 2tx): input (2ty, 2tx) only when the
+    // footprint starts at the input's origin, i.e. the depthwise pad is 0 (3x3 s2); a 5x5 s2 block
+    // with a pooled shortcut (pad 1) runs unfused
+    if (d.g.res_mode == 2 && (d.stride != 2 || pl != 0 || d.g.r_W != d.in.W)) return nullptr;
     const bool co16 = d.g.M <= 16;
     if (d.k == 3 && d.stride == 1) return co16 ? ir_go<3, 1, 16>(e, d, s) : ir_go<3, 1, 32>(e, d, s);
     if (d.k == 3 && d.stride == 2) return co16 ? ir_go<3, 2, 16>(e, d, s) : ir_go<3, 2, 32>(e, d, s);

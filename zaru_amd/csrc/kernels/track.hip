@@ -334,16 +334,17 @@ __global__ __launch_bounds__(64) void hand_manage_kernel(const HandManageParams 
 
 }  // namespace
 
-// one workgroup: a block-wide exclusive scan of the request flags per 1024-stream chunk
-__global__ __launch_bounds__(1024) void due_compact_kernel(const int32_t *pending, int S, const ViewDesc tmpl,
-                                                           int32_t *due, int32_t *ndue, ViewDesc *due_views,
-                                                           uint64_t *total) {
+// one workgroup: a block-wide exclusive scan of the request flags per 1024-stream chunk; the
+// flags are pending[s] != 0, or (lost_of != null) the streams whose tracker holds no RoI
+__global__ __launch_bounds__(1024) void due_compact_kernel(const int32_t *pending, const TrackState *lost_of, int S,
+                                                           const ViewDesc tmpl, int32_t *due, int32_t *ndue,
+                                                           ViewDesc *due_views, uint64_t *total) {
     __shared__ int wsum[16];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     int base = 0;
     for (int c0 = 0; c0 < S; c0 += 1024) {
         const int s = c0 + t;
-        const bool req = s < S && pending[s] != 0;
+        const bool req = s < S && (lost_of ? lost_of[s].active == 0 : pending[s] != 0);
         const uint64_t m = __ballot(req);
         const int in_wave = (int)__popcll(m & ((1ull << lane) - 1ull));
         if (lane == 0) wsum[w] = (int)__popcll(m);
@@ -369,10 +370,59 @@ __global__ __launch_bounds__(1024) void due_compact_kernel(const int32_t *pendin
     }
 }
 
-const char *launch_due_compact(const int32_t *det_pending, int S, const ViewDesc &tmpl, int32_t *due, int32_t *ndue,
-                               ViewDesc *due_views, uint64_t *total, hipStream_t s) {
-    hipLaunchKernelGGL(due_compact_kernel, dim3(1), dim3(1024), 0, s, det_pending, S, tmpl, due, ndue, due_views, total);
+const char *launch_due_compact(const int32_t *det_pending, const TrackState *lost_of, int S, const ViewDesc &tmpl,
+                               int32_t *due, int32_t *ndue, ViewDesc *due_views, uint64_t *total, hipStream_t s) {
+    hipLaunchKernelGGL(due_compact_kernel, dim3(1), dim3(1024), 0, s, det_pending, lost_of, S, tmpl, due, ndue,
+                       due_views, total);
     return "due_compact_kernel";
+}
+
+// Rust's f32::total_cmp key (TotalF32, num.rs): the bits with the magnitude flipped for negatives,
+// compared as signed integers
+__device__ __forceinline__ int32_t total_key(float v) {
+    const int32_t b = __float_as_int(v);
+    return b ^ (int32_t)((uint32_t)(b >> 31) >> 1);
+}
+
+// One thread per stream: examples/facemesh.rs:45-54 after `tracker.track` returned None.  A
+// stream whose tracker holds no RoI ran this frame's detection (its slot of count / dets); if it
+// found any face, the RoI becomes the bounding rect of the most confident detection --
+// `max_by_key(TotalF32(confidence))`, which keeps the LAST of equal maxima -- unrotated and
+// unpadded (LandmarkTracker::set_roi), and the next frame's view is derived from it.
+__global__ __launch_bounds__(256) void reseed_kernel(const ReseedParams P) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s >= P.N) return;
+    TrackState st = P.state[s];
+    if (st.active) return;  // tracked this frame: no detection ran for it
+    const int cnt = min(P.count[s], P.dcap);
+    if (cnt <= 0) return;   // nothing detected: still lost, the next frame detects again
+    const float *d = P.dets + (int64_t)s * P.dcap * 20;
+    int best = 0;
+    int32_t bk = total_key(d[0]);
+    for (int k = 1; k < cnt; ++k) {
+        const int32_t key = total_key(d[k * 20]);
+        if (key >= bk) {  // >=: the last maximum
+            bk = key;
+            best = k;
+        }
+    }
+    const float *b = d + best * 20;
+    st.roi[0] = b[2];
+    st.roi[1] = b[3];
+    st.roi[2] = b[4];
+    st.roi[3] = b[5];
+    st.roi[4] = 0.f;
+    st.active = 1;
+    st.frame_w = P.fsize[2 * s];
+    st.frame_h = P.fsize[2 * s + 1];
+    next_view(st, P.views[s], s, P.asp_w, P.asp_h);
+    P.state[s] = st;
+    if (P.reseeded) atomicAdd((unsigned long long *)P.reseeded, 1ull);
+}
+
+const char *launch_reseed(const ReseedParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(reseed_kernel, dim3((p.N + 255) / 256), dim3(256), 0, s, p);
+    return "reseed_kernel";
 }
 
 const char *launch_hand_manage(const HandManageParams &p, hipStream_t s) {

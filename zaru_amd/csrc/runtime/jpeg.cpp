@@ -286,7 +286,12 @@ struct zr_jpeg_decoder {
 };
 
 namespace {
-int err(int code, const std::string &m) { return zr_internal::set_error(code, m); }
+// every ZR_ERR_DEVICE here is a failed HIP call: its last-error slot is consumed with the
+// return, so the failure is reported once (session.cpp's HIP_TRY does the same)
+int err(int code, const std::string &m) {
+    if (code == ZR_ERR_DEVICE) (void)hipGetLastError();
+    return zr_internal::set_error(code, m);
+}
 
 
 // Frame layout + entropy decoding shared by the device decode and the host coefficient dump.
@@ -910,13 +915,16 @@ int zr_jpeg_decode_batch_async(zr_jpeg_decoder *dec, size_t n, const uint8_t *co
             sp.changed = reinterpret_cast<int *>(dec->d_sync);
             static_assert((zr::JS_PASSES + 1) * sizeof(int) <= 256, "change counters");
             if (hipMemsetAsync(dec->d_sync, 0, 256, st) != hipSuccess) return err(ZR_ERR_DEVICE, "jpeg: counter reset failed");
-            // ZARU_JPEG_SYNC_PASSES (0..JS_PASSES, read per call): fewer sync passes, so the tests
-            // can send frames through the serial finish
-            const char *pe = std::getenv("ZARU_JPEG_SYNC_PASSES");
-            const int passes = pe ? std::max(0, std::min(zr::JS_PASSES, (int)std::strtol(pe, nullptr, 10))) : zr::JS_PASSES;
+            // ZARU_JPEG_SYNC_PASSES (0..JS_PASSES, read once per process): fewer sync passes, so
+            // the tests can send frames through the serial finish
+            static const int passes = [] {
+                const char *pe = std::getenv("ZARU_JPEG_SYNC_PASSES");
+                return pe ? std::max(0, std::min(zr::JS_PASSES, (int)std::strtol(pe, nullptr, 10))) : zr::JS_PASSES;
+            }();
             for (int pass = 0; pass <= passes; pass++) zr::launch_jpeg_sync_scan(sp, pass, st);
             zr::launch_jpeg_sync_finish(sp, st);
-            if (const char *dump = std::getenv("ZARU_JPEG_SYNC_DUMP")) {  // diagnostics: the first sync frame's states
+            static const char *const dump_path = std::getenv("ZARU_JPEG_SYNC_DUMP");  // read once
+            if (const char *dump = dump_path) {  // diagnostics: the first sync frame's states
                 const zr::JpegSyncFrame &F0 = sfr[0];
                 std::vector<int> cnt(64);
                 std::vector<zr::JpegSyncState> xs(F0.nseg);

@@ -57,11 +57,16 @@ int guarded(F &&body) noexcept {
     }
 }
 
+// A failed HIP call is returned to the caller once: the thread's last-error slot, which the
+// failing call also set, is consumed here, so the next entry point (zr_comm_*'s pending-error
+// check, the kernel-launch checks below) does not report the same, already returned failure again.
 #define HIP_TRY(expr)                                                                    \
     do {                                                                                 \
         hipError_t e_ = (expr);                                                          \
-        if (e_ != hipSuccess)                                                            \
+        if (e_ != hipSuccess) {                                                          \
+            (void)hipGetLastError();                                                     \
             return set_err(ZR_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+        }                                                                                \
     } while (0)
 
 // One set of scratch buffers + a private stream.  Sessions keep a small pool so concurrent
@@ -341,8 +346,10 @@ int zr_session_create(const uint8_t *onnx, size_t len, const uint32_t *out_sel, 
         std::vector<uint32_t> sel(out_sel, out_sel + n_sel);
         if (!zr::compile_plan(m, sel, s->plan, err)) return set_err(ZR_ERR_MODEL, err);
         int ndev = 0;
-        if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+            (void)hipGetLastError();  // returned here, as HIP_TRY does
             return set_err(ZR_ERR_DEVICE, "no HIP device " + std::to_string(device));
+        }
         HIP_TRY(hipSetDevice(device));
         const size_t wb = s->plan.weights.size() * sizeof(float);
         HIP_TRY(hipMalloc((void **)&s->weights, wb ? wb : 4));
@@ -863,8 +870,50 @@ int zr_due_compact_async(const int32_t *d_det_pending, size_t n, const zr_view_d
         if (!d_det_pending || !view_template || !d_due || !d_ndue || !d_due_views)
             return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument");
         if (n == 0 || n > (1u << 24)) return set_err(ZR_ERR_INVALID_ARGUMENT, "bad stream count");
-        zr::launch_due_compact(d_det_pending, (int)n, *reinterpret_cast<const zr::ViewDesc *>(view_template), d_due,
-                               d_ndue, reinterpret_cast<zr::ViewDesc *>(d_due_views), d_total, (hipStream_t)hip_stream);
+        zr::launch_due_compact(d_det_pending, nullptr, (int)n, *reinterpret_cast<const zr::ViewDesc *>(view_template),
+                               d_due, d_ndue, reinterpret_cast<zr::ViewDesc *>(d_due_views), d_total,
+                               (hipStream_t)hip_stream);
+        HIP_TRY(hipGetLastError());
+        return ZR_OK;
+    });
+}
+
+int zr_track_lost_compact_async(const zr_track_state *d_state, size_t n, const zr_view_desc *view_template,
+                                int32_t *d_due, int32_t *d_ndue, zr_view_desc *d_due_views, uint64_t *d_total,
+                                void *hip_stream) {
+    return guarded([&]() -> int {
+        if (!d_state || !view_template || !d_due || !d_ndue || !d_due_views)
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument");
+        if (n == 0 || n > (1u << 24)) return set_err(ZR_ERR_INVALID_ARGUMENT, "bad stream count");
+        zr::launch_due_compact(nullptr, reinterpret_cast<const zr::TrackState *>(d_state), (int)n,
+                               *reinterpret_cast<const zr::ViewDesc *>(view_template), d_due, d_ndue,
+                               reinterpret_cast<zr::ViewDesc *>(d_due_views), d_total, (hipStream_t)hip_stream);
+        HIP_TRY(hipGetLastError());
+        return ZR_OK;
+    });
+}
+
+int zr_track_reseed_best_async(const int32_t *d_count, const float *d_dets, size_t dcap, const uint32_t *d_frame_size,
+                               size_t n, const zr_track_cfg *cfg, zr_track_state *d_state, zr_view_desc *d_views,
+                               uint64_t *d_reseeded, void *hip_stream) {
+    return guarded([&]() -> int {
+        if (!d_count || !d_dets || !d_frame_size || !cfg || !d_state || !d_views || dcap == 0)
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "null argument");
+        if (n == 0) return ZR_OK;
+        if (cfg->aspect_w <= 0 || cfg->aspect_h <= 0 || n > (1u << 24) || dcap > 65536)
+            return set_err(ZR_ERR_INVALID_ARGUMENT, "bad re-seeding configuration");
+        zr::ReseedParams p{};
+        p.count = d_count;
+        p.dets = d_dets;
+        p.dcap = (int)dcap;
+        p.fsize = d_frame_size;
+        p.N = (int)n;
+        p.asp_w = cfg->aspect_w;
+        p.asp_h = cfg->aspect_h;
+        p.state = reinterpret_cast<zr::TrackState *>(d_state);
+        p.views = reinterpret_cast<zr::ViewDesc *>(d_views);
+        p.reseeded = d_reseeded;
+        zr::launch_reseed(p, (hipStream_t)hip_stream);
         HIP_TRY(hipGetLastError());
         return ZR_OK;
     });
@@ -1082,6 +1131,7 @@ int zr_event_query(void *event) {
     return guarded([&]() -> int {
         const hipError_t e = hipEventQuery((hipEvent_t)event);
         if (e == hipSuccess) return ZR_OK;
+        (void)hipGetLastError();  // not-ready is no failure; a failure is returned here, once
         if (e == hipErrorNotReady) return 1;
         return set_err(ZR_ERR_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
     });

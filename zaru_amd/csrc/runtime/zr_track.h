@@ -111,10 +111,25 @@ struct HandManageParams {
     int asp_w, asp_h;
 };
 const char *launch_hand_manage(const HandManageParams &p, hipStream_t s);
-// The streams whose detection hand_manage requested (det_pending[s] != 0), in stream order: due[k]
-// = s for k < *ndue, and due_views[k] = the template view with frame = s (one workgroup).
-const char *launch_due_compact(const int32_t *det_pending, int S, const ViewDesc &tmpl, int32_t *due, int32_t *ndue,
-                               ViewDesc *due_views, uint64_t *total, hipStream_t s);
+// The streams whose detection hand_manage requested (det_pending[s] != 0), or -- lost_of != null
+// -- whose tracker state holds no RoI (active == 0), in stream order: due[k] = s for k < *ndue,
+// and due_views[k] = the template view with frame = s (one workgroup).
+const char *launch_due_compact(const int32_t *det_pending, const TrackState *lost_of, int S, const ViewDesc &tmpl,
+                               int32_t *due, int32_t *ndue, ViewDesc *due_views, uint64_t *total, hipStream_t s);
+// The face video loop's re-seeding (examples/facemesh.rs:45-54): a stream without RoI takes the
+// bounding rect of its most confident detection (the last of equal maxima) as its RoI.
+struct ReseedParams {
+    const int *count;        // [N] detections of this frame's detection (det_post, mapped)
+    const float *dets;       // [N][dcap][20]
+    int dcap;
+    const uint32_t *fsize;   // [N][2] frame width, height
+    int N;
+    int asp_w, asp_h;        // landmark network aspect ratio
+    TrackState *state;       // [N] in / out
+    ViewDesc *views;         // [N] out: the next estimate's view of a re-seeded stream
+    uint64_t *reseeded;      // running count of re-seeded streams (may be null)
+};
+const char *launch_reseed(const ReseedParams &p, hipStream_t s);
 
 // fn: 0 sinf, 1 cosf, 2 expf, 3 atanf, 4 atan2f(a, b) -- glibc_math.h on the device
 const char *launch_glibc_math(int fn, const float *a, const float *b, float *out, int64_t n, hipStream_t s);
