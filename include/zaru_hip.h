@@ -150,7 +150,8 @@ int zr_comm_create(const uint8_t id[128], int nranks, int rank, int device, zr_c
 void zr_comm_destroy(zr_comm *c);
 /* the communicator's rank count (what an all-gather writes nranks * bytes for) */
 int zr_comm_size(const zr_comm *c, int *nranks);
-/* recv (nranks * bytes, rank-major) <- every rank's send (bytes), enqueued on hip_stream.
+/* recv (nranks * bytes, rank-major) <- every rank's send (bytes), enqueued on hip_stream (not NULL:
+ * the legacy default stream is refused with ZR_ERR_INVALID_ARGUMENT).
  * Every zr_comm_* call first takes the thread's pending HIP error (hipGetLastError) and, if one
  * is set, returns ZR_ERR_DEVICE naming it without calling RCCL; after an RCCL call it clears
  * only the status RCCL itself left. */

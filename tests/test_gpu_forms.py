@@ -47,6 +47,7 @@ SWITCHES = {
     "no_rt": "-rt",
     "no_ir": "-ir",
     "no_irl": "-irl",
+    "no_wsp": "-wsp",
     "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws,-groups,-dwgap,-rt,-ir,-irl",
 }
 
@@ -218,3 +219,41 @@ def test_irl2_form_is_bitwise_neutral(tmp_path):
     for k in res["default"]:
         if k != "kernels":
             assert np.array_equal(res["default"][k], res["no_irl2"][k]), (k, float(np.abs(res["default"][k] - res["no_irl2"][k]).max()))
+
+
+# The warp-specialized form on BlazePalm's 5x5 stride-1 blocks (form "wsp": 24^2 x 128, 12^2 / 6^2
+# x 256 channels) at the bench's palm batches: 85 frames (the hand line's sub-batches) and 256.
+WSP_CHILD = r"""
+import sys, ctypes as C, numpy as np
+sys.path.insert(0, sys.argv[1])
+from zaru_amd.nn import NeuralNetwork, model_bytes
+from zaru_amd._lib import lib, check
+out, kernels = {}, []
+net = NeuralNetwork.from_onnx(model_bytes("palm_detection_lite")).load()
+check(lib().zr_profile_enable(net._h, 1))
+for b in (85, 256):
+    x = np.random.default_rng(b).uniform(-1.0, 1.0, size=(b, 3, 192, 192)).astype(np.float32)
+    for i, o in enumerate(net.estimate(x)):
+        out[f"{b}/{i}"] = o
+need = C.c_size_t()
+buf = C.create_string_buffer(1 << 20)
+check(lib().zr_profile_read(net._h, buf, len(buf), C.byref(need)))
+kernels += [l.split()[0] for l in buf.value.decode().splitlines() if l.strip()]
+np.savez(sys.argv[2], kernels=np.array(kernels), **out)
+"""
+
+
+def test_wsp_form_is_bitwise_neutral(tmp_path):
+    res = {}
+    for name, env in (("default", ""), ("no_wsp", "-wsp")):
+        path = str(tmp_path / f"{name}.npz")
+        subprocess.run([sys.executable, "-c", WSP_CHILD, REPO, path], env=dict(os.environ, ZARU_HIP_FORMS=env),
+                       check=True, timeout=110)
+        with np.load(path) as z:
+            res[name] = {k: z[k] for k in z.files}
+    ws = {k for k in res["default"]["kernels"] if k.startswith("dwpw_ws_kernel")}
+    assert {"dwpw_ws_kernel<5,1,12,4,2,3>", "dwpw_ws_kernel<5,1,6,4,2,3>"} <= ws, ws
+    assert not any(k.startswith("dwpw_ws_kernel") for k in res["no_wsp"]["kernels"])
+    for k in res["default"]:
+        if k != "kernels":
+            assert np.array_equal(res["default"][k], res["no_wsp"][k]), (k, float(np.abs(res["default"][k] - res["no_wsp"][k]).max()))

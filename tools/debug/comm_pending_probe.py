@@ -13,7 +13,8 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path.insert(0, REPO)
+# ZARU_PROBE_ROOT: import zaru_amd from another tree (alt/r05: the round-5 build, package + .so)
+sys.path.insert(0, os.path.join(REPO, os.environ["ZARU_PROBE_ROOT"]) if os.environ.get("ZARU_PROBE_ROOT") else REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
 
@@ -22,7 +23,19 @@ def main():
     ap.add_argument("--stream", choices=["null", "real"], default="null")
     ap.add_argument("--gathers", type=int, default=2)
     ap.add_argument("--skip-destroy", action="store_true")
+    ap.add_argument("--repeat", type=int, default=1, help="replay the whole sequence this many times")
+    ap.add_argument("--force-pending", action="store_true",
+                    help="leave a HIP error pending before the gathers (hipSetDevice(9999) through ctypes), as the "
+                         "round-5 library's unconsumed memcpy2d failure did")
     a = ap.parse_args()
+    for it in range(a.repeat):
+        print(f"=== iteration {it}", flush=True)
+        if not one(a, it):
+            print("STALE ERROR REPRODUCED", flush=True)
+            break
+
+
+def one(a, it):
     import numpy as np
     from zaru_amd._lib import Comm, DeviceBuffer, lib, synchronize
     hip = C.CDLL(os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib", "libamdhip64.so"))
@@ -47,6 +60,8 @@ def main():
         peek("zr_stream_create")
     rc = lib().zr_memcpy2d_async(dst.ptr, 4, src.ptr, 256, 256, 1, 2, None)
     peek(f"zr_memcpy2d_async(pitch < width) rc={rc}")
+    if a.force_pending:
+        peek(f"hipSetDevice(9999) rc={hip.hipSetDevice(9999)}")
     for k in range(a.gathers):
         try:
             comm.all_gather_async(src.ptr, dst.ptr, 256, st)
@@ -61,6 +76,9 @@ def main():
     e = hip.hipDeviceSynchronize()
     peek(f"hipDeviceSynchronize rc={e}")
     import zaru_amd.host as H
+    H.set_models_dir(os.path.join(REPO, "zaru_amd", "models"))
+    if it == 0:
+        print("zaru_amd from", os.path.dirname(H.__file__), flush=True)
     W, Hh, NF = 1920, 1080, 2
     f = np.random.default_rng(1).integers(0, 256, size=(NF, Hh, W, 4), dtype=np.uint8)
     buf = DeviceBuffer.from_array(f)
@@ -70,14 +88,17 @@ def main():
     peek("pipeline created")
     p.set_frames(flist, [[] for _ in range(NF)])
     peek("set_frames")
+    ok = True
     try:
         p.run_frames()
         peek("run_frames ok")
     except Exception as ex:  # noqa: BLE001
         peek(f"run_frames raised {ex}")
+        ok = False
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(REPO, "gpurun_out", f"comm_probe_{a.stream}.json"), "w") as fh:
+    with open(os.path.join(REPO, "gpurun_out", f"comm_probe_{a.stream}_{it}.json"), "w") as fh:
         json.dump(log, fh, indent=1)
+    return ok
 
 
 if __name__ == "__main__":

@@ -119,6 +119,11 @@ int zr_comm_all_gather_async(zr_comm *c, const void *d_send, void *d_recv, size_
     return guarded([&]() -> int {
         if (!c || !c->comm || !d_send || !d_recv)
             return zr_internal::set_error(ZR_ERR_INVALID_ARGUMENT, "null communicator or buffer");
+        // the gather runs on a stream of the caller's pipeline; the legacy NULL stream (which
+        // waits for, and blocks, every blocking stream of the device, and which RCCL's stream
+        // bookkeeping treats as a special case) is refused
+        if (!hip_stream)
+            return zr_internal::set_error(ZR_ERR_INVALID_ARGUMENT, "the all-gather needs a HIP stream (not the NULL stream)");
         if (int e = pending_hip_error("zr_comm_all_gather_async")) return e;
         if (bytes == 0) return ZR_OK;
         // bytes as ncclChar elements: the records are opaque 32-bit words (f32 and u32 bits)

@@ -198,7 +198,8 @@ struct DwPwParams {
 //   dwgap: depthwise + global average pool in one launch (plan.cpp fuse_dw_gap)
 //   rt: row-task depthwise inside the LDS-DMA MFMA dwpw (dwpw_dma_body, RT > 0)
 //   ir: expand 1x1 + depthwise + projection in one launch (plan.cpp mark_inverted_residuals, ir.hip)
-enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_VRES, FORM_VSTORE, FORM_WS, FORM_GROUPS, FORM_DWGAP, FORM_RT, FORM_IR, FORM_IRL, FORM_IRL2, FORM_COUNT };
+//   wsp: the warp-specialized form also for BlazePalm's 24^2 / 12^2 / 6^2 5x5 blocks (dwpw_ws.hip)
+enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_VRES, FORM_VSTORE, FORM_WS, FORM_GROUPS, FORM_DWGAP, FORM_RT, FORM_IR, FORM_IRL, FORM_IRL2, FORM_WSP, FORM_COUNT };
 bool form_on(Form f);
 
 bool stem_supported(int cin, int k, int stride, int cout);
