@@ -47,7 +47,7 @@ SWITCHES = {
     "no_rt": "-rt",
     "no_ir": "-ir",
     "no_irl": "-irl",
-    "no_wsp": "-wsp",
+    "no_bneck": "-bneck",
     "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws,-groups,-dwgap,-rt,-ir,-irl",
 }
 
@@ -176,8 +176,9 @@ def test_rt_form_is_bitwise_neutral_at_bench_batches(tmp_path):
         with np.load(path) as z:
             res[name] = {k: z[k] for k in z.files}
     widths = {k.rsplit(",", 1)[-1].rstrip(">") for k in res["default"]["kernels"] if k.startswith("dwpw_dma")}
-    # row tasks of 2 (12^2 / 6^2 / 14^2 / 28^2), 4 (palm 48^2) and 8 (FaceMesh / BlazeFace 3x3)
-    assert {"2", "4", "8"} <= widths, widths
+    # row tasks of 2 (12^2 / 6^2 / 14^2 / 28^2) and 4 (palm 48^2, FaceMesh 24^2: the MTW-2 layouts
+    # are capped at 4 since round 6, rt_hi)
+    assert {"2", "4"} <= widths, widths
     assert {k.rsplit(",", 1)[-1].rstrip(">") for k in res["no_rt"]["kernels"] if k.startswith("dwpw_dma")} == {"0"}
     for k in res["default"]:
         if k != "kernels":
@@ -221,18 +222,19 @@ def test_irl2_form_is_bitwise_neutral(tmp_path):
             assert np.array_equal(res["default"][k], res["no_irl2"][k]), (k, float(np.abs(res["default"][k] - res["no_irl2"][k]).max()))
 
 
-# The warp-specialized form on BlazePalm's 5x5 stride-1 blocks (form "wsp": 24^2 x 128, 12^2 / 6^2
-# x 256 channels) at the bench's palm batches: 85 frames (the hand line's sub-batches) and 256.
-WSP_CHILD = r"""
+# FaceMesh V2's bottleneck blocks in one launch (form "bneck": the C -> C/2 reduction, the 3x3
+# depthwise, the 1x1 back to C and the residual; 128^2 / 64^2 / 32^2 planes) at a small batch and
+# at the face_next line's sub-batch (512 frames in 3 sub-batches).
+BNECK_CHILD = r"""
 import sys, ctypes as C, numpy as np
 sys.path.insert(0, sys.argv[1])
 from zaru_amd.nn import NeuralNetwork, model_bytes
 from zaru_amd._lib import lib, check
 out, kernels = {}, []
-net = NeuralNetwork.from_onnx(model_bytes("palm_detection_lite")).load()
+net = NeuralNetwork.from_onnx(model_bytes("face_landmarks_detector")).load()
 check(lib().zr_profile_enable(net._h, 1))
-for b in (85, 256):
-    x = np.random.default_rng(b).uniform(-1.0, 1.0, size=(b, 3, 192, 192)).astype(np.float32)
+for b in (7, 171):
+    x = np.random.default_rng(b).uniform(-1.0, 1.0, size=(b, 3, 256, 256)).astype(np.float32)
     for i, o in enumerate(net.estimate(x)):
         out[f"{b}/{i}"] = o
 need = C.c_size_t()
@@ -243,17 +245,17 @@ np.savez(sys.argv[2], kernels=np.array(kernels), **out)
 """
 
 
-def test_wsp_form_is_bitwise_neutral(tmp_path):
+def test_bneck_form_is_bitwise_neutral(tmp_path):
     res = {}
-    for name, env in (("default", ""), ("no_wsp", "-wsp")):
+    for name, env in (("default", ""), ("no_bneck", "-bneck")):
         path = str(tmp_path / f"{name}.npz")
-        subprocess.run([sys.executable, "-c", WSP_CHILD, REPO, path], env=dict(os.environ, ZARU_HIP_FORMS=env),
+        subprocess.run([sys.executable, "-c", BNECK_CHILD, REPO, path], env=dict(os.environ, ZARU_HIP_FORMS=env),
                        check=True, timeout=110)
         with np.load(path) as z:
             res[name] = {k: z[k] for k in z.files}
-    ws = {k for k in res["default"]["kernels"] if k.startswith("dwpw_ws_kernel")}
-    assert {"dwpw_ws_kernel<5,1,12,4,2,3>", "dwpw_ws_kernel<5,1,6,4,2,3>"} <= ws, ws
-    assert not any(k.startswith("dwpw_ws_kernel") for k in res["no_wsp"]["kernels"])
+    used = {k for k in res["default"]["kernels"] if k.startswith("bneck_kernel")}
+    assert used == {"bneck_kernel<16,128>", "bneck_kernel<32,64>", "bneck_kernel<64,32>"}, used
+    assert not any(k.startswith("bneck_kernel") for k in res["no_bneck"]["kernels"])
     for k in res["default"]:
         if k != "kernels":
-            assert np.array_equal(res["default"][k], res["no_wsp"][k]), (k, float(np.abs(res["default"][k] - res["no_wsp"][k]).max()))
+            assert np.array_equal(res["default"][k], res["no_bneck"][k]), (k, float(np.abs(res["default"][k] - res["no_bneck"][k]).max()))

@@ -612,10 +612,12 @@ static int dfkc_for(int wgs, int cin) {
 // holds all of its padding) and an even R (8-byte aligned windows: even W and run starts).
 // the widest row task an instance is built for: DFKC * BN / 256, capped where the window and the
 // K^2 weights would cost occupancy next to the accumulators (5x5 at MTW = 1 and MTW >= 3: 2, else 8).
-// 5x5 at MTW = 2: 4 (the palm 48^2 blocks: 219 -> 210 us at 256 frames; an 8-wide task's lanes
-// read windows 32 B apart, 4-way bank conflicts; profiles/r05_layers/)
+// MTW = 2: 4 (an 8-wide task's lanes read windows 32 B apart: 4-way bank conflicts on ds_read_b64;
+// 4-wide, 16 B apart: 2-way.  The palm 48^2 5x5 blocks: 219 -> 210 us at 256 frames,
+// profiles/r05_layers/; FaceMesh's 24^2 3x3 blocks: 48.1 / 47.8 -> 43.9 / 42.3 us at 256 images,
+// profiles/r06_layers/face_landmark_256_rtcap4_vs_8.txt; 2-wide tasks there: per-output form, slower)
 constexpr int rt_hi(int K, int MTW, int r) {
-    return r < 2 ? 2 : (MTW == 1 && K == 5) || MTW >= 3 ? 2 : K == 5 && MTW == 2 && r > 4 ? 4 : r > 8 ? 8 : r;
+    return r < 2 ? 2 : (MTW == 1 && K == 5) || MTW >= 3 ? 2 : MTW == 2 && r > 4 ? 4 : r > 8 ? 8 : r;
 }
 
 // A/B knob (bitwise neutral, like the form switches): ZARU_HIP_RT_CAP = the widest row task

@@ -342,18 +342,6 @@ __global__ __launch_bounds__(512) void dwpw_ws_kernel(const DwPwParams P, const 
     }
 }
 
-// the fewest column tiles a launch needs for the persistent form: about one per CU where the
-// 1x1 is no heavier than the depthwise work (the hand shapes), an eighth of the CUs for the
-// MFMA-heavy 256-row palm blocks (ZARU_HIP_WS_MINTILES overrides both, for sweeps)
-static int ws_min_tiles(int ncu, int mtw) {
-    static const int env = [] {
-        const char *e = std::getenv("ZARU_HIP_WS_MINTILES");
-        return e ? (int)std::strtol(e, nullptr, 10) : -1;
-    }();
-    if (env >= 0) return env;
-    return mtw >= 2 ? ncu / 8 : (ncu * 4 + 4) / 5;
-}
-
 template <int K, int S, int R, int WM, int MTW, int NTW>
 const char *ws_go(const DwPwParams &p, hipStream_t s, bool launch) {
     constexpr int FC = WS_FC, BN = (4 / WM) * NTW * 32, KKP = (FC * K * K + 3) / 4 * 4;
@@ -381,7 +369,7 @@ const char *ws_go(const DwPwParams &p, hipStream_t s, bool launch) {
     }();
     // a persistent workgroup per CU pays off only with about a tile per CU or more (at 341 hand
     // ROIs the 7^2 layers have 75 tiles: 2.2x slower than the per-tile form)
-    if (L.nct < ws_min_tiles(ncu, MTW)) return nullptr;
+    if (L.nct * 5 < ncu * 4) return nullptr;
     L.rq = rm / 4;
     const int slots = FC * L.rq + KKP / 4 + 2 * (FC / 4);
     L.stg = (slots + 63) / 64 * 256;
@@ -411,17 +399,10 @@ bool ws_enabled() { return form_on(FORM_WS); }  // ZARU_HIP_FORMS=-ws: the per-t
 // Mpad <= 64 -> 2 x 2 waves, <= 128 -> 4 x 1; N tiles per wave so a tile holds whole rows.
 #define ZR_WS64(K, S, R, NT) if (mp <= 64) return ws_go<K, S, R, 2, 1, NT>(p, s, launch);
 #define ZR_WS128(K, S, R, NT) if (mp <= 128) return ws_go<K, S, R, 4, 1, NT>(p, s, launch);
-#define ZR_WS256(K, S, R, NT) if (mp <= 256) return ws_go<K, S, R, 4, 2, NT>(p, s, launch);
 
 const char *ws_dispatch(const DwPwParams &p, hipStream_t s, bool launch) {
     const int mp = p.g.Mpad, ow = p.OW;
-    // BlazePalm's 5x5 stride-1 blocks (form wsp): 24^2 x 128 and 12^2 / 6^2 x 256 channels, 96-column
-    // tiles of whole rows; there the 1x1 is 5-10x the depthwise work, so the matrix waves stay fed
-    if (form_on(FORM_WSP) && p.k == 5 && p.stride == 1 && mp > 128) {
-        if (ow == 12) { ZR_WS256(5, 1, 12, 3) }
-        if (ow == 6) { ZR_WS256(5, 1, 6, 3) }
-    }
-    if (form_on(FORM_WSP) && p.k == 5 && p.stride == 1 && ow == 24) { ZR_WS128(5, 1, 24, 3) }
+
     if (p.k == 3 && p.stride == 1 && ow == 14) { ZR_WS64(3, 1, 14, 7) }
     if (p.k == 5 && p.stride == 1 && ow == 14) { ZR_WS64(5, 1, 14, 7) }
     if (p.k == 5 && p.stride == 1 && ow == 7) { ZR_WS128(5, 1, 7, 7) }
@@ -430,7 +411,6 @@ const char *ws_dispatch(const DwPwParams &p, hipStream_t s, bool launch) {
 }
 #undef ZR_WS64
 #undef ZR_WS128
-#undef ZR_WS256
 
 }  // namespace
 

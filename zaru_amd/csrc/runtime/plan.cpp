@@ -1258,6 +1258,7 @@ void run_plan(const Plan &plan, const Binding &b, hipStream_t stream, LaunchHook
             if (hook) hook->before(stream);
             const char *kname = launch_ir(ge, dp, stream);
             if (!kname) kname = launch_irl(ge, dp, stream);
+            if (!kname) kname = launch_bneck(ge, dp, stream);
             if (kname) {
                 // fused-boundary bytes: the block input (+ residual) and the output
                 const double bytes = s.bytes + s2.bytes - 8.0 * (double)s.out.C * s.out.H * s.out.W;

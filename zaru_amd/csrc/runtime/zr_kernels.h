@@ -198,8 +198,8 @@ struct DwPwParams {
 //   dwgap: depthwise + global average pool in one launch (plan.cpp fuse_dw_gap)
 //   rt: row-task depthwise inside the LDS-DMA MFMA dwpw (dwpw_dma_body, RT > 0)
 //   ir: expand 1x1 + depthwise + projection in one launch (plan.cpp mark_inverted_residuals, ir.hip)
-//   wsp: the warp-specialized form also for BlazePalm's 24^2 / 12^2 / 6^2 5x5 blocks (dwpw_ws.hip)
-enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_VRES, FORM_VSTORE, FORM_WS, FORM_GROUPS, FORM_DWGAP, FORM_RT, FORM_IR, FORM_IRL, FORM_IRL2, FORM_WSP, FORM_COUNT };
+//   bneck: FaceMesh V2's reduction 1x1 + depthwise + 1x1 + residual in one launch (bneck.hip)
+enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_VRES, FORM_VSTORE, FORM_WS, FORM_GROUPS, FORM_DWGAP, FORM_RT, FORM_IR, FORM_IRL, FORM_IRL2, FORM_BNECK, FORM_COUNT };
 bool form_on(Form f);
 
 bool stem_supported(int cin, int k, int stride, int cout);
@@ -237,5 +237,8 @@ const char *launch_dwpw_mfma_group(const DwPwParams *p, int n, hipStream_t s);
 const char *launch_ir(const GemmParams &e, const DwPwParams &d, hipStream_t s);
 // the same for the low-resolution blocks (irl.hip: a workgroup per image plane)
 const char *launch_irl(const GemmParams &e, const DwPwParams &d, hipStream_t s);
+// FaceMesh V2's bottleneck pair (a C -> C/2 reduction feeding a 3x3 dwpw back to C with the
+// reduction's input as residual) in one launch (bneck.hip); nullptr when the shapes do not fit
+const char *launch_bneck(const GemmParams &e, const DwPwParams &d, hipStream_t s);
 
 }  // namespace zr
