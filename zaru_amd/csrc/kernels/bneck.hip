@@ -3,7 +3,7 @@
 // (+ bias), the block input added back and a PReLU.  Reference: the Conv / PRelu / Add nodes of
 // face_landmarks_detector.onnx that ORT / tract execute at crates/zaru/src/nn/mod.rs:483-533
 // (face/landmark/mediapipe.rs:81-115; the plan's `gemm (ir=1) -> dwpw res=1` pairs, 14 of them at
-// 128^2 / 64^2 / 32^2 with C = 16 / 32 / 64).
+// 128^2 / 64^2 / 32^2 with C = 16 / 32 / 64; fused here: the 128^2 and 64^2 ones).
 //
 // Unfused, the reduction writes C/2 planes to HBM and the dwpw launch reads them back and reads
 // the block input again for the residual: 4C floats per position against the block's 2C.  Here a
@@ -132,7 +132,7 @@ const char *bneck_go(const GemmParams &e, const DwPwParams &d, hipStream_t s) {
 // The fused form applies to a reduction (1x1, C -> C/2, no residual, CNHW input) whose output only
 // the next 3x3 stride-1 depthwise -> 1x1 (C/2 -> C) step reads, with that step's residual the
 // reduction's input (res_mode 1, every channel), TF-style 'same' padding over a square plane of
-// width 128, 64 or 32 (the band holds whole rows), and plain CNHW outputs.
+// width 128 or 64 (the band holds whole rows), and plain CNHW outputs.
 const char *launch_bneck(const GemmParams &e, const DwPwParams &d, hipStream_t s) {
     const int C = e.K, W = d.in.W;
     if (!form_on(FORM_BNECK) || e.KK != 1 || e.res_mode != 0 || e.post.kind != ACT_NONE || e.M * 2 != C ||
@@ -145,7 +145,9 @@ const char *launch_bneck(const GemmParams &e, const DwPwParams &d, hipStream_t s
         return nullptr;
     if (C == 16 && W == 128) return bneck_go<16, 128>(e, d, s);
     if (C == 32 && W == 64) return bneck_go<32, 64>(e, d, s);
-    if (C == 64 && W == 32) return bneck_go<64, 32>(e, d, s);
+    // (C = 64 at 32^2 measured slower than the two launches: 68-71 vs 52 us at 171 images -- the
+    // VALU reduction of 64 channels and 3 waves per SIMD cost more than the saved round trip;
+    // profiles/r06_layers/face_landmarks_detector_171_bneck_vs_unfused.txt)
     return nullptr;
 }
 

@@ -321,9 +321,11 @@ __global__ __launch_bounds__(256) void dwpw_valu_kernel(const DwPwParams P, int 
 // index is static.  Same arithmetic, same order as dwpw_valu_kernel.
 // WL: the layer's weights are staged in LDS (see below) -- for launches of few tiles, where each
 // CU's scalar cache is cold for every channel; otherwise they come through the scalar cache.
-template <int K, int S, int CO, int VF, int RES, bool WL>
+// NB: staging buffers -- 2: the next chunk's DMA in flight while one computes; 3 (form vres3):
+// two chunks in flight, the wait counted so the newer one stays outstanding across the barrier.
+template <int K, int S, int CO, int VF, int RES, bool WL, int NB = 2>
 __global__ __launch_bounds__(256) void dwpw_vres_kernel(const DwPwParams P, int tpi, int ntiles, int bufsz, int lw) {
-    extern __shared__ __attribute__((aligned(16))) float sIn[];  // two buffers of [VF * rows][lw]
+    extern __shared__ __attribute__((aligned(16))) float sIn[];  // NB buffers of [VF * rows][lw]
     constexpr int NCH = (CO + VF - 1) / VF, PL = DwPad<K, S>::L, DMAX = 6, VT = VTQ, NW = 4;
     const GemmParams &G = P.g;
     const int cpx = gridDim.x >> 3;  // gridDim.x is a multiple of 8
@@ -397,7 +399,7 @@ __global__ __launch_bounds__(256) void dwpw_vres_kernel(const DwPwParams P, int 
     // returns, so the compiler can run loads ahead under lgkmcnt(N)); scalar loads there would
     // share lgkmcnt and, returning out of order, force lgkmcnt(0) per channel.
     constexpr int RS = (K * K + 1 + 3) / 4 * 4;
-    float *sW = sIn + 2 * bufsz, *sD = sW + Cin * CO;
+    float *sW = sIn + NB * bufsz, *sD = sW + Cin * CO;
     if constexpr (WL) {
     for (int i = tid; i < Cin * CO; i += 64 * NW) {
         const int k = i / CO, m = i - k * CO;
@@ -409,17 +411,28 @@ __global__ __launch_bounds__(256) void dwpw_vres_kernel(const DwPwParams P, int 
     }
     }
     stage_dma(0, sIn);
+    if (NB == 3 && VF < Cin) stage_dma(VF, sIn + bufsz);
+    const int cnt_w = nwi > wave ? (nwi - wave + NW - 1) / NW : 0;  // DMA instructions of this wave per chunk
 
 #pragma unroll
     for (int j = 0; j < NCH; ++j) {
         const int kc = j * VF;
         if (kc >= Cin) break;
-        const float *buf = sIn + (j & 1) * bufsz;
-        // every wave's DMA of chunk j has landed (explicit: the barrier alone does not promise
-        // it), then chunk j - 1's readers are done with the other buffer
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (kc + VF < Cin) stage_dma(kc + VF, sIn + ((j + 1) & 1) * bufsz);
+        const float *buf = sIn + (j % NB) * bufsz;
+        if constexpr (NB == 2) {
+            // every wave's DMA of chunk j has landed (explicit: the barrier alone does not
+            // promise it), then chunk j - 1's readers are done with the other buffer
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (kc + VF < Cin) stage_dma(kc + VF, sIn + ((j + 1) & 1) * bufsz);
+        } else {
+            // chunk j has landed (chunk j + 1's DMA, issued after it, may stay in flight), then the
+            // barrier -- LDS traffic only -- hands it over; chunk j - 1's readers are done with the
+            // buffer chunk j + 2 goes to
+            wait_vmcnt_dyn(kc + VF < Cin ? cnt_w : 0);
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (kc + 2 * VF < Cin) stage_dma(kc + 2 * VF, sIn + ((j + 2) % NB) * bufsz);
+        }
         // one channel: depthwise from the staged taps, residual capture, 1x1 accumulation
         auto chan = [&](int c, int ch) {
             const float *t0 = buf + c * R * lw + lb;
@@ -525,7 +538,13 @@ const char *dwpw_vres_go(const DwPwParams &p, hipStream_t s) {
     dim3 grid((ntiles + 7) / 8 * 8);
     constexpr int mode = S;  // vres_mode: centre tap at stride 1, 2x2 pool at stride 2
     const bool wl = ntiles < 2048;  // measured: LDS weights win below ~8 tiles per CU, lose above
-    const size_t lds = sizeof(float) * (2 * (size_t)bufsz + (wl ? (size_t)p.g.K * (CO + (K * K + 4) / 4 * 4) : 0));
+    // form vres3: a third staging buffer (two chunks in flight) where three still fit 64 KiB
+    const bool nb3 = form_on(FORM_VRES3) && !wl && vf8 && 3 * sizeof(float) * (size_t)bufsz <= 64 * 1024;
+    const size_t lds = sizeof(float) * ((nb3 ? 3 : 2) * (size_t)bufsz + (wl ? (size_t)p.g.K * (CO + (K * K + 4) / 4 * 4) : 0));
+    if (nb3) {
+        hipLaunchKernelGGL((dwpw_vres_kernel<K, S, CO, VFKC, mode, false, 3>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
+        return kernel_name("dwpw_vres_kernel<%d,%d,%d,%d,%d,false,3>", K, S, CO, VFKC, mode);
+    }
     if (wl) {
         if (vf8) hipLaunchKernelGGL((dwpw_vres_kernel<K, S, CO, VFKC, mode, true>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
         else hipLaunchKernelGGL((dwpw_vres_kernel<K, S, CO, 4, mode, true>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
@@ -533,7 +552,7 @@ const char *dwpw_vres_go(const DwPwParams &p, hipStream_t s) {
         if (vf8) hipLaunchKernelGGL((dwpw_vres_kernel<K, S, CO, VFKC, mode, false>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
         else hipLaunchKernelGGL((dwpw_vres_kernel<K, S, CO, 4, mode, false>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
     }
-    return kernel_name("dwpw_vres_kernel<%d,%d,%d,%d,%d,%s>", K, S, CO, vf, mode, wl ? "true" : "false");
+    return kernel_name("dwpw_vres_kernel<%d,%d,%d,%d,%d,%s,2>", K, S, CO, vf, mode, wl ? "true" : "false");
 }
 
 template <int K, int S, int CO>
@@ -555,7 +574,13 @@ const char *dwpw_valu_go(const DwPwParams &p, hipStream_t s) {
     const int vres = vres_mode(p, S, CO);
     const bool db = form_on(FORM_VALU_DB) && (CO == 16 || CO == 32 || (CO == 48 && (S == 2 || vres))) &&
                     2 * sizeof(float) * (size_t)buf_of(4) <= 64 * 1024;
-    const bool small = db && !(CO == 32 && fit8);
+    // ZARU_HIP_VALU_WIDE=1 (A/B knob): 8-channel chunks also for 16 output channels when the layer
+    // has >= 32 input channels (fewer dependent DMA round trips per tile)
+    static const bool wide16 = [] {
+        const char *e = std::getenv("ZARU_HIP_VALU_WIDE");
+        return e && *e == '1';
+    }();
+    const bool small = db && !(CO == 32 && fit8) && !(wide16 && CO == 16 && p.g.K >= 32 && fit8);
     const int vf = small ? 4 : VFKC;
     const int bufsz = buf_of(vf);
     dim3 grid((ntiles + 7) / 8 * 8);
