@@ -48,8 +48,7 @@ SWITCHES = {
     "no_ir": "-ir",
     "no_irl": "-irl",
     "no_bneck": "-bneck",
-    "no_vres3": "-vres3",
-    "no_irlpad": "-irlpad",
+    "no_vres5": "-vres5",
     "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws,-groups,-dwgap,-rt,-ir,-irl",
 }
 

@@ -49,7 +49,7 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // NI: images per workgroup (2 at 7^2: each M wave then runs two independent MFMA chains, and a
 // few hundred ROIs fill the CUs in one round instead of one and a third)
 template <int K, int HW, int S, int CX, int MP, int NI>
-__global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPwParams D, int tpcp) {
+__global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPwParams D) {
     constexpr int HO = HW / S, P = HW * HW, PO = HO * HO, PL = S == 1 ? K / 2 : K / 2 - 1;
     constexpr int PH = (HO - 1) * S + K, PW = (PH + 1) & ~1, PP = PH * PW;  // padded plane (even rows)
     constexpr int NE = (P + 15) / 16, NET = NI * NE, NEW = (NET + 3) / 4;   // expand column tiles (per M wave)
@@ -108,15 +108,10 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
     const Bounds eb = bounds(E.pre), db = bounds(D.dw_act);  // (E.post: none, host-checked)
 
     // ---- D waves: channel dc of a chunk, outputs dx0 .. dx0 + RW - 1 of row dy
-    // tpcp (host-chosen, >= HO * RPR): task slots per channel.  Padded to 16 at 14^2 (form irlpad:
-    // 14 row tasks + 2 idle lanes), a half-wave's 8-byte window reads then cover two channels'
-    // 14 rows exactly once -- rows 18 floats apart and planes 324 apart put them on disjoint bank
-    // pairs -- where 14 tasks per channel let a third channel's rows collide with the first's
-    const int dt = tid - 256, ntp = IRL_CEC * tpcp;
-    const int dj = !mrole && dt < NI * ntp ? dt / ntp : 0, dtj = dt - dj * ntp;  // image dj of the workgroup
-    const int dc = dtj / tpcp, dr = dtj - dc * tpcp;
-    const bool dw_on = !mrole && dt < NI * ntp && dr < HO * RPR;
-    const int dy = dr / RPR, dx0 = (dr - dy * RPR) * RW;
+    const int dt = tid - 256;
+    const bool dw_on = !mrole && dt < NI * NTASK;
+    const int dj = dw_on ? dt / NTASK : 0, dtj = dt - dj * NTASK;  // image dj of the workgroup
+    const int dc = dw_on ? dtj / (HO * RPR) : 0, dr = dtj - dc * HO * RPR, dy = dr / RPR, dx0 = (dr - dy * RPR) * RW;
     // The D waves stage every weight through LDS, loaded a step ahead into registers and stored
     // in the step before their use; the M waves then issue no memory loads in the step loop
     // (the compiler's vmcnt waits for operand registers loaded one or two steps earlier counted
@@ -293,9 +288,7 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
 template <int K, int HW, int S, int CX, int MP, int NI = 1>
 const char *irl_go(const GemmParams &e, const DwPwParams &d, hipStream_t s) {
     const int N = d.g.ncols / ((HW / S) * (HW / S));
-    constexpr int HO = HW / S, RW = IRL_CEC * HO * 2 <= 256 && HO % 2 == 0 ? HO / 2 : HO, TPC = HO * (HO / RW);
-    const int tpcp = form_on(FORM_IRLPAD) && TPC == 14 && IRL_CEC * 16 * NI <= 256 ? 16 : TPC;
-    hipLaunchKernelGGL((irl_kernel<K, HW, S, CX, MP, NI>), dim3((N + NI - 1) / NI), dim3(512), 0, s, e, d, tpcp);
+    hipLaunchKernelGGL((irl_kernel<K, HW, S, CX, MP, NI>), dim3((N + NI - 1) / NI), dim3(512), 0, s, e, d);
     return NI == 1 ? kernel_name("irl_kernel<%d,%d,%d,%d,%d>", K, HW, S, CX, MP)
                    : kernel_name("irl_kernel<%d,%d,%d,%d,%d,%d>", K, HW, S, CX, MP, NI);
 }
