@@ -49,6 +49,7 @@ SWITCHES = {
     "no_irl": "-irl",
     "no_bneck": "-bneck",
     "no_vres5": "-vres5",
+    "no_ring3": "-ring3",
     "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws,-groups,-dwgap,-rt,-ir,-irl",
 }
 
@@ -176,11 +177,13 @@ def test_rt_form_is_bitwise_neutral_at_bench_batches(tmp_path):
                        check=True, timeout=110)
         with np.load(path) as z:
             res[name] = {k: z[k] for k in z.files}
-    widths = {k.rsplit(",", 1)[-1].rstrip(">") for k in res["default"]["kernels"] if k.startswith("dwpw_dma")}
+    def rt(k):  # dwpw_dma_kernel<K,S,WM,MTW,DFKC,RT,NB> / dwpw_dma_group_kernel<K,S,WM,MTW,DFKC,RT>
+        return k.split("<", 1)[1].rstrip(">").split(",")[5]
+    widths = {rt(k) for k in res["default"]["kernels"] if k.startswith("dwpw_dma")}
     # row tasks of 2 (12^2 / 6^2 / 14^2 / 28^2) and 4 (palm 48^2, FaceMesh 24^2: the MTW-2 layouts
     # are capped at 4 since round 6, rt_hi)
     assert {"2", "4"} <= widths, widths
-    assert {k.rsplit(",", 1)[-1].rstrip(">") for k in res["no_rt"]["kernels"] if k.startswith("dwpw_dma")} == {"0"}
+    assert {rt(k) for k in res["no_rt"]["kernels"] if k.startswith("dwpw_dma")} == {"0"}
     for k in res["default"]:
         if k != "kernels":
             assert np.array_equal(res["default"][k], res["no_rt"][k]), (k, float(np.abs(res["default"][k] - res["no_rt"][k]).max()))
