@@ -48,8 +48,6 @@ SWITCHES = {
     "no_ir": "-ir",
     "no_irl": "-irl",
     "no_bneck": "-bneck",
-    "no_vres5": "-vres5",
-    "no_ring3": "-ring3",
     "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws,-groups,-dwgap,-rt,-ir,-irl",
 }
 
@@ -177,7 +175,7 @@ def test_rt_form_is_bitwise_neutral_at_bench_batches(tmp_path):
                        check=True, timeout=110)
         with np.load(path) as z:
             res[name] = {k: z[k] for k in z.files}
-    def rt(k):  # dwpw_dma_kernel<K,S,WM,MTW,DFKC,RT,NB> / dwpw_dma_group_kernel<K,S,WM,MTW,DFKC,RT>
+    def rt(k):  # dwpw_dma_kernel / dwpw_dma_group_kernel<K,S,WM,MTW,DFKC,RT>
         return k.split("<", 1)[1].rstrip(">").split(",")[5]
     widths = {rt(k) for k in res["default"]["kernels"] if k.startswith("dwpw_dma")}
     # row tasks of 2 (12^2 / 6^2 / 14^2 / 28^2) and 4 (palm 48^2, FaceMesh 24^2: the MTW-2 layouts

@@ -9,4 +9,6 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
   --steps 20 --warmup 5 --no-cpu-baseline --no-traffic $NOSIDE > $O/bench_prof.json 2> $O/prof.err && \
 ZARU_BENCH_SHARE_GPU=1 timeout -k 10 400 python bench.py --gpus 2 --steps 50 --warmup 10 --no-cpu-baseline \
   --no-traffic --no-profile $NOSIDE > $O/n2.json 2> $O/n2.err && \
+ZARU_BENCH_SHARE_GPU=1 timeout -k 10 400 python bench.py --gpus 2 --workload both --steps 10 --warmup 3 \
+  --no-cpu-baseline --no-traffic --no-profile > $O/n2_both.json 2> $O/n2_both.err && \
 bash tools/gpu_pmc_models.sh ${1:-r06z}_pmc face_detection_short_range:256 face_landmark:256 hand_landmark_lite:341 palm_detection_lite:256

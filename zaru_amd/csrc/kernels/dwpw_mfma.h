@@ -267,11 +267,7 @@ __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) 
 // outside the image reads a zeroed LDS block, the first / last segment of a row zeroes its PL / PR
 // window floats.  The arithmetic is the per-output form's: bias + fmaf over the taps in (ky, kx)
 // order, masked taps as fmaf(w, 0, a) -- so the bits are too (tests/test_gpu_forms.py, -rt).
-// NB = 3 (form ring3, the 5x5 MTW-2 layouts: BlazePalm's 12^2 / 6^2 blocks): a third staging
-// buffer, two chunks in flight; each wave waits only for its own DMA of the chunk about to be
-// read (counted vmcnt), then an LDS-only barrier.  (Round 5's 4-deep ring took a workgroup per CU;
-// three buffers of these layouts still leave two.)
-template <int K, int S, int WM, int MTW, int DFKC, int RT, int NB = 2>
+template <int K, int S, int WM, int MTW, int DFKC, int RT>
 __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int runmax, int bufsz, int bx, int by, int gx) {
     constexpr int WN = 4 / WM, BN = WN * 32, BM = WM * MTW * 32, KK = K * K;
     constexpr int CPAR = 256 / BN, PER = DFKC / CPAR;
@@ -281,7 +277,7 @@ __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int 
     // to pad_t * W + pad_l words before it, into the guard rather than out of the allocation
     extern __shared__ __attribute__((aligned(16))) float lds_all[];
     float *smem = lds_all + 256;
-    float *sD = smem + NB * bufsz;
+    float *sD = smem + 2 * bufsz;
     const GemmParams &G = P.g;
 
     const int cpx = gx >> 3;  // the grid's x extent is a multiple of 8
@@ -413,25 +409,14 @@ __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int 
         for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
     float wa[WT][WS], wnx[WT][WS];
-    static_assert(NB == 2 || !WREG, "the three-buffer ring stages the 1x1 weights by DMA");
     stage(0, smem);
-    if (NB == 3 && DFKC < Cin) stage(DFKC, smem + bufsz);
-    const int cnt_w = nwi > wave ? (nwi - wave + 3) / 4 : 0;  // DMA instructions of this wave per stage
     wload(0, wa);
     for (int kc = 0, it = 0; kc < Cin; kc += DFKC, ++it) {
-        const float *buf = smem + (NB == 2 ? (it & 1) : it % NB) * bufsz;
-        if constexpr (NB == 2) {
-            __syncthreads();  // vmcnt(0) + barrier: this chunk has landed; last chunk's readers are done
-            if (kc + DFKC < Cin) {
-                stage(kc + DFKC, smem + ((it + 1) & 1) * bufsz);
-                wload(kc + DFKC, wnx);
-            }
-        } else {
-            // this chunk has landed (the next one, issued after it, may stay in flight); the
-            // buffer the chunk after next goes to was read by the previous chunk, done by now
-            wait_vmcnt_dyn(kc + DFKC < Cin ? cnt_w : 0);
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            if (kc + 2 * DFKC < Cin) stage(kc + 2 * DFKC, smem + ((it + 2) % NB) * bufsz);
+        const float *buf = smem + (it & 1) * bufsz;
+        __syncthreads();  // vmcnt(0) + barrier: this chunk has landed; last chunk's readers are done
+        if (kc + DFKC < Cin) {
+            stage(kc + DFKC, smem + ((it + 1) & 1) * bufsz);
+            wload(kc + DFKC, wnx);
         }
         const float *sIn = buf, *sW = buf + DFKC * runmax, *sDW = sW + (WREG ? 0 : DFKC * BM), *sDB = sDW + KKP;
         if constexpr (RT > 0) {
@@ -541,10 +526,10 @@ __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int 
 template <int K, int WM, int MTW> constexpr int dma_waves(int rt) {
     return MTW == 1 || (MTW == 2 && K == 3) ? 4 : rt > 0 ? 2 : 1;
 }
-template <int K, int S, int WM, int MTW, int DFKC, int RT, int NB = 2>
+template <int K, int S, int WM, int MTW, int DFKC, int RT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_waves<K, WM, MTW>(RT))))
 void dwpw_dma_kernel(const DwPwParams P, int nct, int runmax, int bufsz) {
-    dwpw_dma_body<K, S, WM, MTW, DFKC, RT, NB>(P, nct, runmax, bufsz, blockIdx.x, blockIdx.y, gridDim.x);
+    dwpw_dma_body<K, S, WM, MTW, DFKC, RT>(P, nct, runmax, bufsz, blockIdx.x, blockIdx.y, gridDim.x);
 }
 
 // sibling layers in one launch (group.h): a0 = nct, a1 = runmax, a2 = bufsz of each part
@@ -656,30 +641,17 @@ template <int K, int S, int WM, int MTW, int DFKC>
 static const char *dma_launch(const DwPwParams &p, dim3 grid, size_t lds, int nct, int runmax, int bufsz, hipStream_t s) {
     constexpr int BN = (4 / WM) * 32, RH = rt_hi(K, MTW, DFKC * BN / 256);
     const int rt = rt_for<K, S>(p, BN, RH);
-    if constexpr (K == 5 && MTW == 2 && WM == 4 && DFKC == 16) {
-        // form ring3: a third staging buffer where it still leaves two workgroups per CU
-        const size_t lds3 = lds + sizeof(float) * (size_t)bufsz;
-        if (form_on(FORM_RING3) && rt == RH && 2 * lds3 <= 160 * 1024) {
-            static const bool attr = hipFuncSetAttribute((const void *)dwpw_dma_kernel<K, S, WM, MTW, DFKC, RH, 3>,
-                                                         hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024) == hipSuccess;
-            if (attr) {
-                hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, DFKC, RH, 3>), grid, dim3(256), lds3, s, p, nct, runmax, bufsz);
-                return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,%d,%d,3>", K, S, WM, MTW, DFKC, RH);
-            }
-            (void)hipGetLastError();  // handled: the two-buffer form below
-        }
-    }
     if (rt == RH) {
         hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, DFKC, RH>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
-        return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,%d,%d,2>", K, S, WM, MTW, DFKC, RH);
+        return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,%d,%d>", K, S, WM, MTW, DFKC, RH);
     }
     if constexpr (RH >= 4)
         if (rt == RH / 2) {
             hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, DFKC, RH / 2>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
-            return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,%d,%d,2>", K, S, WM, MTW, DFKC, RH / 2);
+            return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,%d,%d>", K, S, WM, MTW, DFKC, RH / 2);
         }
     hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, DFKC, 0>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
-    return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,%d,0,2>", K, S, WM, MTW, DFKC);
+    return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,%d,0>", K, S, WM, MTW, DFKC);
 }
 
 template <int K, int S, int WM, int MTW>

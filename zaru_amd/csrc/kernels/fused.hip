@@ -321,10 +321,8 @@ __global__ __launch_bounds__(256) void dwpw_valu_kernel(const DwPwParams P, int 
 // index is static.  Same arithmetic, same order as dwpw_valu_kernel.
 // WL: the layer's weights are staged in LDS (see below) -- for launches of few tiles, where each
 // CU's scalar cache is cold for every channel; otherwise they come through the scalar cache.
-// WPE: the waves per SIMD the register allocation must allow (1: no constraint; 5: form vres5,
-// 5 workgroups per CU instead of 4 for the 32-channel 3x3 blocks -- more chunks in flight)
-template <int K, int S, int CO, int VF, int RES, bool WL, int WPE = 1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void dwpw_vres_kernel(const DwPwParams P, int tpi, int ntiles, int bufsz, int lw) {
+template <int K, int S, int CO, int VF, int RES, bool WL>
+__global__ __launch_bounds__(256) void dwpw_vres_kernel(const DwPwParams P, int tpi, int ntiles, int bufsz, int lw) {
     extern __shared__ __attribute__((aligned(16))) float sIn[];  // two buffers of [VF * rows][lw]
     constexpr int NCH = (CO + VF - 1) / VF, PL = DwPad<K, S>::L, DMAX = 6, VT = VTQ, NW = 4;
     const GemmParams &G = P.g;
@@ -355,11 +353,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const int total = VF * R * srow;
     const int nwi = (total + 63) >> 6, lane = tid & 63, wave = tid >> 6;
     const bool pre_off = nwi <= NW * DMAX;
-    // per DMA slot of this lane: its offset from the chunk's first channel plane and its channel
-    // in the chunk, packed as offset * 8 + channel (-1: a zero slot; VF <= 8 and offsets < 2^28,
-    // host-checked) -- one register per slot instead of two
-    static_assert(VF <= 8, "packed slot channel");
-    int gpk[DMAX];
+    int goff[DMAX], gch[DMAX];
 #pragma unroll
     for (int m = 0; m < DMAX; ++m) {
         const int sl = (wave + NW * m) * 64 + lane;
@@ -367,7 +361,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const int c = qdiv(cr, R, inv_R), r = cr - c * R;
         const int iy = iy_a + r, xv = sx - 1;
         const bool ok = sl < total && iy >= 0 && iy < H && xv >= 0 && 4 * xv < W;
-        gpk[m] = ok ? (int)((((uint32_t)c * (uint32_t)P.in.sC + nbase + (uint32_t)(iy * W + 4 * xv)) << 3) | (uint32_t)c) : -1;
+        goff[m] = ok ? (int)((uint32_t)c * (uint32_t)P.in.sC + nbase + (uint32_t)(iy * W + 4 * xv)) : -1;
+        gch[m] = c;
     }
     auto stage_dma = [&](int kc, float *dst) {
         if (pre_off) {
@@ -377,9 +372,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             for (int m = 0; m < DMAX; ++m) {
                 const int wi = wave + NW * m;
                 if (wi < nwi) {
-                    const int g = gpk[m];
-                    const bool ok = g >= 0 && (g & 7) < cl;
-                    const float *src = ok ? base + ((uint32_t)g >> 3) : (const float *)&zr_zero4;
+                    const bool ok = goff[m] >= 0 && gch[m] < cl;
+                    const float *src = ok ? base + (uint32_t)goff[m] : (const float *)&zr_zero4;
                     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
                                                      (__attribute__((address_space(3))) void *)(dst + wi * 256), 16, 0, 0);
                 }
@@ -500,10 +494,6 @@ namespace {
 // max-pool from the taps, 0 = not applicable.
 static int vres_mode(const DwPwParams &p, int S, int CO) {
     const GemmParams &g = p.g;
-    // (the DMA slot offsets are packed as offset * 8 + channel in 31 bits: 8 channel planes plus
-    // the batch must stay below 2^28 floats)
-    if ((uint64_t)8 * (uint64_t)p.in.sC + (uint64_t)p.in.sN * (uint64_t)(g.ncols / std::max(1, g.P)) >= (1ull << 28))
-        return 0;
     if (!form_on(FORM_VRES) || g.res_mode == 0 || g.r != p.in.p || g.r_sN != p.in.sN || g.r_sC != p.in.sC ||
         g.K > CO || g.r_C > g.K || p.dw_act.kind != ACT_NONE)
         return 0;
@@ -530,22 +520,12 @@ const char *dwpw_vres_go(const DwPwParams &p, hipStream_t s) {
     auto buf_of = [&](int vf) { return (vf * rmax * lw + 255) / 256 * 256; };  // whole 1 KiB DMA rows
     // 8-channel chunks for 32 channels where two buffers fit 64 KiB (as measured for
     // dwpw_valu_kernel), else 4
-    // ZARU_HIP_VRES48_VF8=1 (A/B knob): 8-channel chunks for the 48-channel blocks too (6 chunks
-    // instead of 12 dependent DMA round trips per tile)
-    static const bool vf8_48 = [] {
-        const char *e = std::getenv("ZARU_HIP_VRES48_VF8");
-        return e && *e == '1';
-    }();
-    const bool vf8 = 2 * sizeof(float) * (size_t)buf_of(VFKC) <= 64 * 1024 && (CO == 32 || (vf8_48 && CO == 48));
+    const bool vf8 = 2 * sizeof(float) * (size_t)buf_of(VFKC) <= 64 * 1024 && CO == 32;
     const int vf = vf8 ? VFKC : 4, bufsz = buf_of(vf);
     dim3 grid((ntiles + 7) / 8 * 8);
     constexpr int mode = S;  // vres_mode: centre tap at stride 1, 2x2 pool at stride 2
     const bool wl = ntiles < 2048;  // measured: LDS weights win below ~8 tiles per CU, lose above
     const size_t lds = sizeof(float) * (2 * (size_t)bufsz + (wl ? (size_t)p.g.K * (CO + (K * K + 4) / 4 * 4) : 0));
-    if (!wl && vf8 && CO == 32 && form_on(FORM_VRES5)) {
-        hipLaunchKernelGGL((dwpw_vres_kernel<K, S, CO, VFKC, mode, false, 5>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
-        return kernel_name("dwpw_vres_kernel<%d,%d,%d,%d,%d,false,5>", K, S, CO, VFKC, mode);
-    }
     if (wl) {
         if (vf8) hipLaunchKernelGGL((dwpw_vres_kernel<K, S, CO, VFKC, mode, true>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
         else hipLaunchKernelGGL((dwpw_vres_kernel<K, S, CO, 4, mode, true>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
@@ -553,7 +533,7 @@ const char *dwpw_vres_go(const DwPwParams &p, hipStream_t s) {
         if (vf8) hipLaunchKernelGGL((dwpw_vres_kernel<K, S, CO, VFKC, mode, false>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
         else hipLaunchKernelGGL((dwpw_vres_kernel<K, S, CO, 4, mode, false>), grid, dim3(256), lds, s, p, tpi, ntiles, bufsz, lw);
     }
-    return kernel_name("dwpw_vres_kernel<%d,%d,%d,%d,%d,%s,1>", K, S, CO, vf, mode, wl ? "true" : "false");
+    return kernel_name("dwpw_vres_kernel<%d,%d,%d,%d,%d,%s>", K, S, CO, vf, mode, wl ? "true" : "false");
 }
 
 template <int K, int S, int CO>

@@ -199,9 +199,7 @@ struct DwPwParams {
 //   rt: row-task depthwise inside the LDS-DMA MFMA dwpw (dwpw_dma_body, RT > 0)
 //   ir: expand 1x1 + depthwise + projection in one launch (plan.cpp mark_inverted_residuals, ir.hip)
 //   bneck: FaceMesh V2's reduction 1x1 + depthwise + 1x1 + residual in one launch (bneck.hip)
-//   vres5: the 32-channel vres dwpw compiled for 5 waves per SIMD
-//   ring3: a third LDS-DMA staging buffer in the MFMA dwpw's 5x5 MTW-2 layouts (BlazePalm 12^2 / 6^2)
-enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_VRES, FORM_VSTORE, FORM_WS, FORM_GROUPS, FORM_DWGAP, FORM_RT, FORM_IR, FORM_IRL, FORM_IRL2, FORM_BNECK, FORM_VRES5, FORM_RING3, FORM_COUNT };
+enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_VRES, FORM_VSTORE, FORM_WS, FORM_GROUPS, FORM_DWGAP, FORM_RT, FORM_IR, FORM_IRL, FORM_IRL2, FORM_BNECK, FORM_COUNT };
 bool form_on(Form f);
 
 bool stem_supported(int cin, int k, int stride, int cout);
