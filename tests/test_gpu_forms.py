@@ -48,8 +48,11 @@ SWITCHES = {
     "no_ir": "-ir",
     "no_irl": "-irl",
     "no_bneck": "-bneck",
-    "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws,-groups,-dwgap,-rt,-ir,-irl",
+    "no_pin": "-pin",
+    "irl_lds0": "",  # + ZARU_HIP_IRL_LDS=0 (EXTRA_ENV): irl's plain LDS layout
+    "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws,-groups,-dwgap,-rt,-ir,-irl,-pin",
 }
+EXTRA_ENV = {"irl_lds0": {"ZARU_HIP_IRL_LDS": "0"}}  # name -> extra environment
 
 
 @pytest.fixture(scope="module")
@@ -60,6 +63,7 @@ def outputs(tmp_path_factory):
         path = str(d / f"{name}.npz")
         e = dict(os.environ)
         e["ZARU_HIP_FORMS"] = env
+        e.update(EXTRA_ENV.get(name, {}))
         subprocess.run([sys.executable, "-c", CHILD, REPO, path], env=e, check=True, timeout=110)
         with np.load(path) as z:
             res[name] = {k: z[k] for k in z.files}

@@ -267,7 +267,15 @@ __global__ __launch_bounds__(256) void dwpw_kernel(const DwPwParams P, int nct) 
 // outside the image reads a zeroed LDS block, the first / last segment of a row zeroes its PL / PR
 // window floats.  The arithmetic is the per-output form's: bias + fmaf over the taps in (ky, kx)
 // order, masked taps as fmaf(w, 0, a) -- so the bits are too (tests/test_gpu_forms.py, -rt).
-template <int K, int S, int WM, int MTW, int DFKC, int RT>
+// RD = 1 (form "pin", dwpw_dma_pin_kernel; a task step RT * S that is a multiple of 4, W % 4 == 0):
+// the window rows are read as whole 16-byte vectors from 16-byte aligned starts (ds_read_b128).
+// Left alone the compiler drops a window's unused first / last float and re-pairs the rest into
+// ds_read2_b32 -- two 4-byte reads per lane, banks mod 32, so lanes whose windows are 16 B apart
+// meet 4-way conflicts; an empty asm that takes each loaded vector whole keeps the full read, and
+// b128's 16-lane groups cover a 256-byte bank row with 16-byte-apart lanes where b64's 32-lane
+// groups wrap it twice (PMC: FaceMesh 24^2 4.33 -> 0.13 conflict cycles per LDS instruction).
+// A 4-wide task also stores its outputs as one ds_write_b128.
+template <int K, int S, int WM, int MTW, int DFKC, int RT, int RD = 0>
 __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int runmax, int bufsz, int bx, int by, int gx) {
     constexpr int WN = 4 / WM, BN = WN * 32, BM = WM * MTW * 32, KK = K * K;
     constexpr int CPAR = 256 / BN, PER = DFKC / CPAR;
@@ -370,9 +378,12 @@ __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int 
     // lanes of a half-wave share a bank).  Per task: the run index of its aligned window start in
     // row ky = 0, the rows inside the image, and whether it is the first / last segment of its row
     constexpr int RTE = RT > 0 ? RT : 1;
-    constexpr int PLx = DwPad<K, S>::L, OFF = PLx & 1;
+    static_assert(RD == 0 || (RTE * S) % 4 == 0, "pinned reads: 16-byte window steps");
+    constexpr bool V16 = RD > 0;                                    // 16-byte window reads
+    constexpr int VW = V16 ? 4 : 2;                                 // floats per window read
+    constexpr int PLx = DwPad<K, S>::L, OFF = V16 ? (4 - PLx % 4) % 4 : PLx & 1;
     constexpr int WW = (RTE - 1) * S + K, PR = WW - RTE * S - PLx;  // window floats, right pad
-    constexpr int NB64 = (OFF + WW + 1) / 2;                        // 8-byte reads per window row
+    constexpr int NB64 = (OFF + WW + VW - 1) / VW;                  // reads per window row
     constexpr int SEGS = BN / RTE, TASKS = DFKC * SEGS, NRT = TASKS > 256 ? TASKS / 256 : 1;
     static_assert(RT == 0 || (RT % 2 == 0 && BN % RT == 0 && SEGS % NRT == 0 && (TASKS <= 256 || TASKS % 256 == 0)),
                   "row-task layout");
@@ -436,12 +447,20 @@ __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int 
 #pragma unroll
                     for (int ky = 0; ky < K; ++ky) {
                         const float *row = ((rt_vm[r] >> ky) & 1u) ? chan + rt_base[r] + ky * W : lds_all;
-                        float x[2 * NB64];
+                        float x[VW * NB64];
 #pragma unroll
                         for (int e = 0; e < NB64; ++e) {
-                            const float2 v = *reinterpret_cast<const float2 *>(row + 2 * e);
-                            x[2 * e] = v.x;
-                            x[2 * e + 1] = v.y;
+                            if constexpr (RD == 0) {
+                                const float2 v = *reinterpret_cast<const float2 *>(row + 2 * e);
+                                x[2 * e] = v.x;
+                                x[2 * e + 1] = v.y;
+                            } else {
+                                typedef float fv __attribute__((ext_vector_type(VW)));
+                                fv v = *reinterpret_cast<const fv *>(row + VW * e);
+                                asm("" : "+v"(v));  // the whole vector: no narrowed / re-paired reads
+#pragma unroll
+                                for (int i = 0; i < VW; ++i) x[VW * e + i] = v[i];
+                            }
                         }
 #pragma unroll
                         for (int e = 0; e < PLx; ++e) x[OFF + e] = rt_first[r] ? 0.f : x[OFF + e];
@@ -454,10 +473,18 @@ __device__ __forceinline__ void dwpw_dma_body(const DwPwParams &P, int nct, int 
                     }
                     apply_act_n<RTE>(P.dw_act, a, [&](int) { return live ? kc + c : Cin - 1; });
                     float *dst = sD + c * BN + (r * SPT + rt_g) * RTE;
+                    if constexpr (RD > 0 && RTE % 4 == 0) {
+                        const bool w = live && rt_ok[r];
 #pragma unroll
-                    for (int o = 0; o < RTE; o += 2)
-                        *reinterpret_cast<float2 *>(dst + o) =
-                            make_float2(live && rt_ok[r] ? a[o] : 0.f, live && rt_ok[r] ? a[o + 1] : 0.f);
+                        for (int o = 0; o < RTE; o += 4)
+                            *reinterpret_cast<float4 *>(dst + o) =
+                                make_float4(w ? a[o] : 0.f, w ? a[o + 1] : 0.f, w ? a[o + 2] : 0.f, w ? a[o + 3] : 0.f);
+                    } else {
+#pragma unroll
+                        for (int o = 0; o < RTE; o += 2)
+                            *reinterpret_cast<float2 *>(dst + o) =
+                                make_float2(live && rt_ok[r] ? a[o] : 0.f, live && rt_ok[r] ? a[o + 1] : 0.f);
+                    }
                 }
             }
         } else {
@@ -531,6 +558,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_waves<K
 void dwpw_dma_kernel(const DwPwParams P, int nct, int runmax, int bufsz) {
     dwpw_dma_body<K, S, WM, MTW, DFKC, RT>(P, nct, runmax, bufsz, blockIdx.x, blockIdx.y, gridDim.x);
 }
+// form "pin": the row-task reads at full width (RD = 1 above)
+template <int K, int S, int WM, int MTW, int DFKC, int RT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_waves<K, WM, MTW>(RT))))
+void dwpw_dma_pin_kernel(const DwPwParams P, int nct, int runmax, int bufsz) {
+    dwpw_dma_body<K, S, WM, MTW, DFKC, RT, 1>(P, nct, runmax, bufsz, blockIdx.x, blockIdx.y, gridDim.x);
+}
 
 // sibling layers in one launch (group.h): a0 = nct, a1 = runmax, a2 = bufsz of each part
 template <int K, int S, int WM, int MTW, int DFKC, int RT>
@@ -562,9 +595,19 @@ static bool v4_ok(const DwPwParams &p) {
 
 // LDS bytes of the DMA form for this layer and tile (0 when it does not apply): the longest
 // input run any BN-column tile needs, rounded to 16 B, and whole 1 KiB DMA wave-instructions.
+// LDS bytes for a channel stride of rm words (0: over the 80 KiB two workgroups per CU leave)
+template <int K, int WM, int MTW, int DFKC>
+static size_t dma_lds(int rm, int *bufsz) {
+    constexpr int BN = (4 / WM) * 32, BM = WM * MTW * 32, KKP = (DFKC * K * K + 3) / 4 * 4;
+    const int words = DFKC * rm + (MTW == 1 ? 0 : DFKC * BM) + KKP + DFKC;  // (WREG: no 1x1 weights)
+    *bufsz = (words + 255) / 256 * 256;
+    const size_t lds = sizeof(float) * (256 + 2 * (size_t)*bufsz + DFKC * BN);
+    return lds <= 80 * 1024 ? lds : 0;
+}
+
 template <int K, int S, int WM, int MTW, int DFKC>
 static size_t dma_plan(const DwPwParams &p, int *runmax, int *bufsz) {
-    constexpr int BN = (4 / WM) * 32, BM = WM * MTW * 32, KKP = (DFKC * K * K + 3) / 4 * 4;
+    constexpr int BN = (4 / WM) * 32;
     const int H = p.in.H, W = p.in.W, Pin = H * W, Pq = p.g.P, OW = p.OW;
     // (runs are rounded out to 16-B ends inside the channel plane: sC % 4 == 0 leaves room)
     if (!form_on(FORM_DMA) || p.in.sN != Pin || p.in.sC % 4 || p.g.K % 4 ||
@@ -579,12 +622,9 @@ static size_t dma_plan(const DwPwParams &p, int *runmax, int *bufsz) {
         rm = std::max(rm, e0 - s0);
         if (na >= 4 && (j0 % Pq) == 0) break;  // the pattern has repeated (whole images seen)
     }
-    const int words = DFKC * rm + (MTW == 1 ? 0 : DFKC * BM) + KKP + DFKC;  // (WREG: no 1x1 weights)
     *runmax = rm;
-    *bufsz = (words + 255) / 256 * 256;
     if (p.pad_t * W + p.pad_l > 256) return 0;  // the guard in front of the buffers
-    const size_t lds = sizeof(float) * (256 + 2 * (size_t)*bufsz + DFKC * BN);
-    return lds <= 80 * 1024 ? lds : 0;
+    return dma_lds<K, WM, MTW, DFKC>(rm, bufsz);
 }
 
 // the widest channel chunk the DMA form may use (ZARU_HIP_DFKC: 16 / 32 / 64, for A/B runs)
@@ -637,21 +677,30 @@ static int rt_for(const DwPwParams &p, int bn, int r_hi) {
     return 0;
 }
 
+template <int K, int S, int WM, int MTW, int DFKC, int RT>
+static const char *dma_go(const DwPwParams &p, dim3 grid, size_t lds, int nct, int runmax, int bufsz, hipStream_t s) {
+    // form "pin" where the task step RT * S makes 16-byte window reads (ds_read_b128: FaceMesh 24^2
+    // 44.7 -> 43.2 us, BlazePalm 48^2 205 -> 192 us, 48 -> 24 172 -> 150 us at 256 frames); the
+    // 8-byte form measured slower than the compiler's own narrowed reads (FaceMesh 12^2 39.7 -> 41.1,
+    // hand 28^2 5x5 146 -> 182 us), so 2-float steps keep dwpw_dma_kernel
+    // (profiles/r06_layers/*_pin_vs_not.txt)
+    if constexpr (RT > 0 && (RT * S) % 4 == 0)
+        if (form_on(FORM_PIN) && p.in.W % 4 == 0) {
+            hipLaunchKernelGGL((dwpw_dma_pin_kernel<K, S, WM, MTW, DFKC, RT>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
+            return kernel_name("dwpw_dma_pin_kernel<%d,%d,%d,%d,%d,%d>", K, S, WM, MTW, DFKC, RT);
+        }
+    hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, DFKC, RT>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
+    return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,%d,%d>", K, S, WM, MTW, DFKC, RT);
+}
+
 template <int K, int S, int WM, int MTW, int DFKC>
 static const char *dma_launch(const DwPwParams &p, dim3 grid, size_t lds, int nct, int runmax, int bufsz, hipStream_t s) {
     constexpr int BN = (4 / WM) * 32, RH = rt_hi(K, MTW, DFKC * BN / 256);
     const int rt = rt_for<K, S>(p, BN, RH);
-    if (rt == RH) {
-        hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, DFKC, RH>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
-        return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,%d,%d>", K, S, WM, MTW, DFKC, RH);
-    }
+    if (rt == RH) return dma_go<K, S, WM, MTW, DFKC, RH>(p, grid, lds, nct, runmax, bufsz, s);
     if constexpr (RH >= 4)
-        if (rt == RH / 2) {
-            hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, DFKC, RH / 2>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
-            return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,%d,%d>", K, S, WM, MTW, DFKC, RH / 2);
-        }
-    hipLaunchKernelGGL((dwpw_dma_kernel<K, S, WM, MTW, DFKC, 0>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
-    return kernel_name("dwpw_dma_kernel<%d,%d,%d,%d,%d,0>", K, S, WM, MTW, DFKC);
+        if (rt == RH / 2) return dma_go<K, S, WM, MTW, DFKC, RH / 2>(p, grid, lds, nct, runmax, bufsz, s);
+    return dma_go<K, S, WM, MTW, DFKC, 0>(p, grid, lds, nct, runmax, bufsz, s);
 }
 
 template <int K, int S, int WM, int MTW>

@@ -41,35 +41,87 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int IRL_CEC = 16;  // expanded channels per chunk
 
+// ZR_IRL_TRACE (tools/debug/irl_trace.sh builds a separate library with it; never the product):
+// lane 0 of every wave of the first IRL_TRACE_WG workgroups stores the shader clock (s_memtime)
+// at the start of each step and where its work ends before the step's barrier, into a device
+// buffer of IRL_TRACE_LAUNCHES launches x IRL_TRACE_WG workgroups x 8 waves x 256 slots (slot 4 t +
+// 2: step t starts, + 3: the M waves' expand / the D waves' staging is issued, + 4: its work ends;
+// 0 / 1: the prologue, 254 / 255: the epilogue).
+#ifdef ZR_IRL_TRACE
+constexpr int IRL_TRACE_WG = 16, IRL_TRACE_LAUNCHES = 32;
+__device__ unsigned long long zr_irl_trace_buf[IRL_TRACE_LAUNCHES * IRL_TRACE_WG * 8 * 256];
+// (the clocks go to LDS during the steps -- a global store there would sit in the wave's vmcnt
+// and delay the next wait for its weight loads -- and to the buffer after the epilogue)
+#define IRL_TS(slot) \
+    if (lane == 0) sT[wave][slot] = __builtin_amdgcn_s_memtime();
+#define IRL_TRACE_ARG , int tslot
+#else
+#define IRL_TS(slot)
+#define IRL_TRACE_ARG
+#endif
+
 // a workgroup barrier that waits for this wave's LDS traffic, not its vector-memory loads
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// LDS layout of an instance (LV > 0): the padded planes' row pitch, their stride and the depthwise
+// tile's channel stride, chosen with tools/lds_banks_irl.py's bank model (MI355X_MICROARCH.md §LDS)
+// over the expand's stores, the row tasks' window reads and their tile stores.  The plain layout
+// (row pitch = the padded width rounded to even, packed planes, NI * NCP tile rows) puts a
+// half-wave's 14 row tasks of one channel on 2-4 bank groups (pitch 16: lanes 64 B apart) and the
+// 4 channels of an expand store 4 * PP apart on the same banks.
+struct IrlLds {
+    int pw, pp, dc;  // row pitch (>= padded width, even), plane pad, tile channel pad (floats)
+};
+// LV 2: for 16-byte window reads (ds_read_b128 from 16-byte aligned rows: pitch and strides % 4
+// == 0).  PMC at 341 ROIs: 1.85-2.93 -> 0.26-0.34 conflict cycles per LDS instruction, and every
+// launch within +-2 us (the step is not bound by LDS banks: profiles/r06_layers/
+// hand_landmark_lite_341_irllds_vs_plain.txt); the stride-2 14^2 block at two images per
+// workgroup spills at this layout (108 -> 140 us) and keeps the plain one.
+constexpr IrlLds irl_lds(int K, int HW, int S, int NI, int LV) {
+    if (LV >= 2) {
+        if (K == 3 && HW == 14 && S == 1) return {20, 24, 4};
+        if (K == 5 && HW == 14 && S == 1) return {20, 48, 4};
+        if (K == 5 && HW == 14 && S == 2) return {20, 16, 8};
+        if (K == 5 && HW == 7 && S == 1) return {12, 16, NI == 1 ? 8 : 4};
+    }
+    return {0, 0, 0};
+}
 
 // HW: input plane side; S: the depthwise stride (TF-style 'same' padding: the output plane is
 // HW / S); CX: block-input channels (the expand's K); MP: 32-row slices of the projection (Mpad / 32);
 // NI: images per workgroup (2 at 7^2: each M wave then runs two independent MFMA chains, and a
-// few hundred ROIs fill the CUs in one round instead of one and a third)
-template <int K, int HW, int S, int CX, int MP, int NI>
-__global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPwParams D) {
+// few hundred ROIs fill the CUs in one round instead of one and a third); LV: the LDS layout
+// (irl_lds; 2: the window rows read as whole 16-byte vectors)
+template <int K, int HW, int S, int CX, int MP, int NI, int LV>
+__global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPwParams D IRL_TRACE_ARG) {
     constexpr int HO = HW / S, P = HW * HW, PO = HO * HO, PL = S == 1 ? K / 2 : K / 2 - 1;
-    constexpr int PH = (HO - 1) * S + K, PW = (PH + 1) & ~1, PP = PH * PW;  // padded plane (even rows)
+    constexpr IrlLds LY = irl_lds(K, HW, S, NI, LV);
+    constexpr int PH = (HO - 1) * S + K, PW0 = (PH + 1) & ~1;
+    constexpr int PW = LY.pw > PW0 ? LY.pw : PW0, PP = PH * PW + LY.pp;  // padded plane (even rows)
     constexpr int NE = (P + 15) / 16, NET = NI * NE, NEW = (NET + 3) / 4;   // expand column tiles (per M wave)
     constexpr int NCT = (PO + 31) / 32, NCP = NCT * 32, NCTT = NI * NCT;    // projection column tiles (per image)
+    constexpr int DCS = NI * NCP + LY.dc;                                   // tile channel stride
     constexpr int CPW = 4 / MP, TPW = (NCTT + CPW - 1) / CPW;          // tile stride, tiles per M wave
     constexpr int KS = CX / 4, KK = K * K, NSW = IRL_CEC * KK + IRL_CEC;
     // depthwise task: RW outputs of a row (a half row when whole rows leave half the D threads idle)
     constexpr int RW = IRL_CEC * HO * 2 <= 256 && HO % 2 == 0 ? HO / 2 : HO, RPR = HO / RW;
-    constexpr int WWIN = ((RW - 1) * S + K + 1) & ~1;  // window floats per input row (even)
+    constexpr int WWIN = LV >= 2 ? ((RW - 1) * S + K + 3) & ~3  // window floats per input row (% 4)
+                                 : ((RW - 1) * S + K + 1) & ~1;  // (even)
     constexpr bool W64 = RW == HO || S == 2;           // 8-byte aligned window starts: 8-byte reads
     constexpr int NTASK = IRL_CEC * HO * RPR;          // depthwise tasks per image
     static_assert(4 % MP == 0 && CX % 4 == 0 && NI * NTASK <= 256 && NE >= 4 && HW % S == 0, "irl layout");
+    static_assert(LV < 2 || (RPR == 1 && PW % 4 == 0 && PP % 4 == 0 && W64), "irl: 16-byte aligned window rows");
     // image j of the workgroup: planes sE[.][j][c], tile columns sD[.][c][j * NCP + q]
     __shared__ __attribute__((aligned(16))) float sE[2][NI * IRL_CEC * PP];  // expanded planes (zero border)
-    __shared__ __attribute__((aligned(16))) float sD[2][IRL_CEC * NI * NCP];  // depthwise tiles
+    __shared__ __attribute__((aligned(16))) float sD[2][IRL_CEC * DCS];  // depthwise tiles
     __shared__ float sW[2][NSW];  // a chunk's depthwise weights, then its biases
     // the M waves' operands of step t in sM[t & 1]: chunk t's expand weights [CX][16] and biases,
     // then chunk t - 2's projection weights [16][MP * 32]
     constexpr int MWA = 0, MB = CX * IRL_CEC, MW2 = MB + IRL_CEC, NSM = MW2 + IRL_CEC * MP * 32;
     __shared__ __attribute__((aligned(16))) float sM[2][NSM];
+#ifdef ZR_IRL_TRACE
+    __shared__ unsigned long long sT[8][256];
+#endif
 
     const GemmParams &G = D.g;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -160,6 +212,7 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
     // the D waves run chunk t - 1's depthwise (sE[(t - 1) & 1] -> sD[(t - 1) & 1]) and stage chunk
     // t's depthwise weights.  One barrier per step hands the buffers over.
     auto step = [&](int t) {
+        IRL_TS(4 * t + 2);
         const float *sm = sM[t & 1];
         if (mrole) {
             if (t < nch) {
@@ -194,13 +247,14 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
                     dcur = dn;
                 }
             }
+            IRL_TS(4 * t + 3);
             if (t >= 2) {
                 // projection: acc += W2[m0 .. m0 + 31][chunk t - 2] x its depthwise tile
                 const float *pd = sD[t & 1];
 #pragma unroll
                 for (int s = 0; s < IRL_CEC / 2; ++s) {
                     const float w2 = sm[MW2 + (2 * s + kh) * (MP * 32) + m0 + pcol];
-                    const float *b = pd + (2 * s + kh) * (NI * NCP) + pcol;
+                    const float *b = pd + (2 * s + kh) * DCS + pcol;
 #pragma unroll
                     for (int i = 0; i < TPW; ++i) {
                         const int ct = ct0 + CPW * i;
@@ -217,8 +271,10 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
                     if (dt + 256 * j < NSW) sW[t & 1][dt + 256 * j] = swr[j];
             }
             store_m(t + 1);  // (read in step t + 1; step t reads the other buffer)
+            IRL_TS(4 * t + 5);
             if (t < nch) load_w(t + 1);
             load_m(t + 2);
+            IRL_TS(4 * t + 3);
             if (t >= 1 && t <= nch && dw_on) {
                 // depthwise of chunk t - 1: RW outputs of one row of one channel, each input row once
                 const float *w = sW[(t - 1) & 1] + dc * KK;
@@ -232,11 +288,21 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
                     const float *row = pe + (dy * S + ky) * PW;
                     float xw[WWIN];
                     if constexpr (W64) {
+                        if constexpr (LV == 2) {
 #pragma unroll
-                        for (int e = 0; e < WWIN / 2; ++e) {
-                            const float2 v = reinterpret_cast<const float2 *>(row)[e];
-                            xw[2 * e] = v.x;
-                            xw[2 * e + 1] = v.y;
+                            for (int e = 0; e < WWIN / 4; ++e) {
+                                f32x4 v = reinterpret_cast<const f32x4 *>(row)[e];
+                                asm("" : "+v"(v));  // (whole: no narrowed / re-paired reads)
+#pragma unroll
+                                for (int i = 0; i < 4; ++i) xw[4 * e + i] = v[i];
+                            }
+                        } else {
+#pragma unroll
+                            for (int e = 0; e < WWIN / 2; ++e) {
+                                const float2 v = reinterpret_cast<const float2 *>(row)[e];
+                                xw[2 * e] = v.x;
+                                xw[2 * e + 1] = v.y;
+                            }
                         }
                     } else {
 #pragma unroll
@@ -249,26 +315,30 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
                         for (int o = 0; o < RW; ++o) a[o] = __builtin_fmaf(wt, xw[o * S + kx], a[o]);
                     }
                 }
-                float *dst = sD[(t - 1) & 1] + dc * (NI * NCP) + dj * NCP + dy * HO + dx0;
+                float *dst = sD[(t - 1) & 1] + dc * DCS + dj * NCP + dy * HO + dx0;
 #pragma unroll
                 for (int o = 0; o < RW; ++o) dst[o] = clamp(db, a[o]);
             }
         }
+        IRL_TS(4 * t + 4);
         lds_barrier();
     };
 
+    IRL_TS(0);
     if (!mrole) {
         load_w(0);
         load_m(0);
         store_m(0);
         load_m(1);
     }
+    IRL_TS(1);
     lds_barrier();  // the zeroed planes, step 0's M operands
     for (int t = 0; t < nch + 2; t += 2) {  // (nch even, host-checked: buffer t & 1 is static)
         step(t);
         step(t + 1);
     }
 
+    IRL_TS(254);
     if (mrole) {
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
@@ -283,12 +353,39 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
             }
         }
     }
+    IRL_TS(255);
+#ifdef ZR_IRL_TRACE
+    if (blockIdx.x < IRL_TRACE_WG)
+        for (int i = lane; i < 256; i += 64)
+            zr_irl_trace_buf[(((tslot % IRL_TRACE_LAUNCHES) * IRL_TRACE_WG + blockIdx.x) * 8 + wave) * 256 + i] = sT[wave][i];
+#endif
+}
+
+#ifdef ZR_IRL_TRACE
+int irl_trace_launches = 0;  // (trace builds: the buffer's launch slot of the next irl launch)
+#endif
+
+// ZARU_HIP_IRL_LDS=0 (A/B knob, bitwise neutral): the plain layout everywhere
+int irl_lds_env() {
+    static const int v = [] {
+        const char *e = std::getenv("ZARU_HIP_IRL_LDS");
+        return e ? (int)std::strtol(e, nullptr, 10) : 2;
+    }();
+    return v;
 }
 
 template <int K, int HW, int S, int CX, int MP, int NI = 1>
 const char *irl_go(const GemmParams &e, const DwPwParams &d, hipStream_t s) {
     const int N = d.g.ncols / ((HW / S) * (HW / S));
-    hipLaunchKernelGGL((irl_kernel<K, HW, S, CX, MP, NI>), dim3((N + NI - 1) / NI), dim3(512), 0, s, e, d);
+    constexpr bool padded = !(S == 2 && NI == 2);
+#ifdef ZR_IRL_TRACE
+#define IRL_TRACE_PASS , irl_trace_launches++
+#else
+#define IRL_TRACE_PASS
+#endif
+    if (padded && irl_lds_env() != 0)
+        hipLaunchKernelGGL((irl_kernel<K, HW, S, CX, MP, NI, padded ? 2 : 0>), dim3((N + NI - 1) / NI), dim3(512), 0, s, e, d IRL_TRACE_PASS);
+    else hipLaunchKernelGGL((irl_kernel<K, HW, S, CX, MP, NI, 0>), dim3((N + NI - 1) / NI), dim3(512), 0, s, e, d IRL_TRACE_PASS);
     return NI == 1 ? kernel_name("irl_kernel<%d,%d,%d,%d,%d>", K, HW, S, CX, MP)
                    : kernel_name("irl_kernel<%d,%d,%d,%d,%d,%d>", K, HW, S, CX, MP, NI);
 }
@@ -305,6 +402,22 @@ int cu_count() {
 }
 
 }  // namespace
+
+#ifdef ZR_IRL_TRACE
+// the trace buffer, for tools/debug/irl_trace.py (trace builds only)
+extern "C" int zr_debug_irl_trace(unsigned long long *dst, size_t n, int clear) {
+    const size_t cap = sizeof(zr_irl_trace_buf) / sizeof(zr_irl_trace_buf[0]);
+    if (n > cap) n = cap;
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpyFromSymbol(dst, HIP_SYMBOL(zr_irl_trace_buf), n * 8, 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    if (clear) {
+        static unsigned long long zero[IRL_TRACE_LAUNCHES * IRL_TRACE_WG * 8 * 256];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(zr_irl_trace_buf), zero, sizeof(zero), 0, hipMemcpyHostToDevice) != hipSuccess) return -1;
+    }
+    return (int)n;
+}
+#endif
 
 // The fused form applies to an expand (1x1, no residual, CNHW input) whose output only the next
 // depthwise -> 1x1 step reads (plan.cpp mark_inverted_residuals), with the models' TF-style

@@ -27,7 +27,7 @@ const char *kernel_name(const char *fmt, ...) {
 
 bool form_on(Form f) {
     static const unsigned mask = [] {
-        static const char *const names[FORM_COUNT] = {"dma", "v4", "valu", "valu_db", "rows", "vres", "vstore", "ws", "groups", "dwgap", "rt", "ir", "irl", "irl2", "bneck"};
+        static const char *const names[FORM_COUNT] = {"dma", "v4", "valu", "valu_db", "rows", "vres", "vstore", "ws", "groups", "dwgap", "rt", "ir", "irl", "irl2", "bneck", "pin"};
         unsigned m = (1u << FORM_COUNT) - 1;
         const char *e = std::getenv("ZARU_HIP_FORMS");
         for (std::string s = e ? e : ""; !s.empty();) {

@@ -199,7 +199,8 @@ struct DwPwParams {
 //   rt: row-task depthwise inside the LDS-DMA MFMA dwpw (dwpw_dma_body, RT > 0)
 //   ir: expand 1x1 + depthwise + projection in one launch (plan.cpp mark_inverted_residuals, ir.hip)
 //   bneck: FaceMesh V2's reduction 1x1 + depthwise + 1x1 + residual in one launch (bneck.hip)
-enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_VRES, FORM_VSTORE, FORM_WS, FORM_GROUPS, FORM_DWGAP, FORM_RT, FORM_IR, FORM_IRL, FORM_IRL2, FORM_BNECK, FORM_COUNT };
+//   pin: the row-task depthwise's window reads at full width (ds_read_b64 / b128, dwpw_dma_pin_kernel)
+enum Form : int { FORM_DMA, FORM_V4, FORM_VALU, FORM_VALU_DB, FORM_ROWS, FORM_VRES, FORM_VSTORE, FORM_WS, FORM_GROUPS, FORM_DWGAP, FORM_RT, FORM_IR, FORM_IRL, FORM_IRL2, FORM_BNECK, FORM_PIN, FORM_COUNT };
 bool form_on(Form f);
 
 bool stem_supported(int cin, int k, int stride, int cout);
