@@ -713,7 +713,10 @@ const char *dwpw_go(const DwPwParams &p, hipStream_t s) {
     if constexpr (K == 3 && MTW == 1) {
         // wider channel chunks: fewer dependent DMA round trips per tile (the 6^2 / 3^2 launches
         // of a few dozen workgroups are nothing but those round trips)
-        const int dk = dfkc_for(nct * mb, p.g.K);
+        // (32-column stride-1 tiles: 32 channels make the row tasks 4 wide, so the window reads
+        // go 16-byte (form pin): FaceMesh 12^2 39.3 / 38.1 -> 35.3 / 34.4 us, BlazeFace 8^2 16-18
+        // -> 14-16 us at 256 images, profiles/r06_layers/*_dfkc32_vs_16.txt)
+        const int dk = S == 1 && WM == 4 && !dfkc_env() && form_on(FORM_PIN) ? 32 : dfkc_for(nct * mb, p.g.K);
         if (dk >= 64)
             if (const size_t lds = dma_plan<K, S, WM, MTW, 64>(p, &runmax, &bufsz))
                 return dma_launch<K, S, WM, MTW, 64>(p, grid, lds, nct, runmax, bufsz, s);
