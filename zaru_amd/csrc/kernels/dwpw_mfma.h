@@ -651,7 +651,9 @@ static int dfkc_for(int wgs, int cin) {
 // segments.  Needs the models' TF-style padding with W = OW * S (so a row's first / last segment
 // holds all of its padding) and an even R (8-byte aligned windows: even W and run starts).
 // the widest row task an instance is built for: DFKC * BN / 256, capped where the window and the
-// K^2 weights would cost occupancy next to the accumulators (5x5 at MTW = 1 and MTW >= 3: 2, else 8).
+// K^2 weights would cost occupancy next to the accumulators (5x5 at MTW = 1 and MTW >= 3: 2, else 8;
+// the hand 28^2 5x5 block at 4-wide 16-byte-read tasks: 145 -> 200 us, profiles/r06_layers/
+// hand_landmark_lite_341_k5rt4_vs_2.txt).
 // MTW = 2: 4 (an 8-wide task's lanes read windows 32 B apart: 4-way bank conflicts on ds_read_b64;
 // 4-wide, 16 B apart: 2-way.  The palm 48^2 5x5 blocks: 219 -> 210 us at 256 frames,
 // profiles/r05_layers/; FaceMesh's 24^2 3x3 blocks: 48.1 / 47.8 -> 43.9 / 42.3 us at 256 images,
