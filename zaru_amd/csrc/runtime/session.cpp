@@ -81,12 +81,12 @@ struct Ctx {
     size_t input_floats = 0;
     uint8_t *image = nullptr;  // host-image upload (zr_cnn_estimate_views)
     size_t image_bytes = 0;
-    zr::ViewDesc *views = nullptr;
-    zr::FrameDesc *frames = nullptr;
-    size_t views_cap = 0, frames_cap = 0;
-    zr::ViewDesc *h_views = nullptr;  // pinned host staging of the descriptors
-    zr::FrameDesc *h_frames = nullptr;
-    size_t h_views_cap = 0, h_frames_cap = 0;
+    // the view and frame descriptors of a launch: one device block [views | frames] and its pinned
+    // host staging, so an upload is one copy (one blit on the stream, not two)
+    uint8_t *desc = nullptr, *h_desc = nullptr;
+    size_t desc_bytes = 0;
+    zr::ViewDesc *views = nullptr;    // (into desc)
+    zr::FrameDesc *frames = nullptr;  // (into desc)
     std::vector<float *> outs;  // device outputs for the synchronous entry points
     std::vector<size_t> outs_floats;
 
@@ -95,10 +95,8 @@ struct Ctx {
         (void)hipFree(arena);
         (void)hipFree(input);
         (void)hipFree(image);
-        (void)hipFree(views);
-        (void)hipFree(frames);
-        (void)hipHostFree(h_views);
-        (void)hipHostFree(h_frames);
+        (void)hipFree(desc);
+        (void)hipHostFree(h_desc);
         for (auto p : outs) (void)hipFree(p);
         if (done) (void)hipEventDestroy(done);
         if (stream) (void)hipStreamDestroy(stream);
@@ -297,33 +295,39 @@ int sync_outputs(zr_session *s, Ctx *c, size_t batch) {
 
 int upload_views(Ctx *c, const zr_frame *frames, size_t nf, const zr_view *views,
                  const uint32_t *view_frame, size_t nv, hipStream_t stream) {
-    if (int rc = grow(c->views, c->views_cap, nv ? nv : 1)) return rc;
-    if (int rc = grow(c->frames, c->frames_cap, nf ? nf : 1)) return rc;
-    // pinned staging: the context was acquired idle (or waited for), so it is free to rewrite,
-    // and the copies stay asynchronous (a pageable source would block the host on the stream)
-    if (c->h_views_cap < nv || c->h_frames_cap < nf) {
-        (void)hipHostFree(c->h_views);
-        (void)hipHostFree(c->h_frames);
-        c->h_views_cap = nv + nv / 2 + 64;
-        c->h_frames_cap = nf + nf / 2 + 64;
-        HIP_TRY(hipHostMalloc((void **)&c->h_views, c->h_views_cap * sizeof(zr::ViewDesc)));
-        HIP_TRY(hipHostMalloc((void **)&c->h_frames, c->h_frames_cap * sizeof(zr::FrameDesc)));
+    // [views | frames], the frames 256-byte aligned.  Pinned staging: the context was acquired idle
+    // (or waited for), so it is free to rewrite, and the copy stays asynchronous (a pageable
+    // source would block the host on the stream)
+    const size_t foff = (nv * sizeof(zr::ViewDesc) + 255) & ~(size_t)255;
+    const size_t bytes = foff + (nf ? nf : 1) * sizeof(zr::FrameDesc);
+    if (c->desc_bytes < bytes) {
+        (void)hipFree(c->desc);
+        (void)hipHostFree(c->h_desc);
+        c->desc = c->h_desc = nullptr;
+        c->desc_bytes = 0;
+        const size_t cap = bytes + bytes / 2 + 4096;
+        HIP_TRY(hipMalloc((void **)&c->desc, cap));
+        HIP_TRY(hipHostMalloc((void **)&c->h_desc, cap));
+        c->desc_bytes = cap;
     }
+    zr::ViewDesc *hv = reinterpret_cast<zr::ViewDesc *>(c->h_desc);
+    zr::FrameDesc *hf = reinterpret_cast<zr::FrameDesc *>(c->h_desc + foff);
+    c->views = reinterpret_cast<zr::ViewDesc *>(c->desc);
+    c->frames = reinterpret_cast<zr::FrameDesc *>(c->desc + foff);
     for (size_t i = 0; i < nv; i++) {
         const uint32_t f = view_frame ? view_frame[i] : 0;
         if (f >= nf) return set_err(ZR_ERR_INVALID_ARGUMENT, "view_frame index out of range");
-        c->h_views[i] = make_view(views[i], f);
+        hv[i] = make_view(views[i], f);
     }
     for (size_t i = 0; i < nf; i++) {
         if (!frames[i].rgba || frames[i].width == 0 || frames[i].height == 0)
             return set_err(ZR_ERR_INVALID_ARGUMENT, "empty frame");
-        c->h_frames[i].rgba = frames[i].rgba;
-        c->h_frames[i].w = frames[i].width;
-        c->h_frames[i].h = frames[i].height;
-        c->h_frames[i].stride = frames[i].row_stride;
+        hf[i].rgba = frames[i].rgba;
+        hf[i].w = frames[i].width;
+        hf[i].h = frames[i].height;
+        hf[i].stride = frames[i].row_stride;
     }
-    HIP_TRY(hipMemcpyAsync(c->views, c->h_views, nv * sizeof(zr::ViewDesc), hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipMemcpyAsync(c->frames, c->h_frames, nf * sizeof(zr::FrameDesc), hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(c->desc, c->h_desc, foff + nf * sizeof(zr::FrameDesc), hipMemcpyHostToDevice, stream));
     return ZR_OK;
 }
 
