@@ -49,10 +49,11 @@ SWITCHES = {
     "no_irl": "-irl",
     "no_bneck": "-bneck",
     "no_pin": "-pin",
-    "irl_lds0": "",  # + ZARU_HIP_IRL_LDS=0 (EXTRA_ENV): irl's plain LDS layout
+    "irl_lds0": "",  # + ZARU_HIP_IRL_LDS (EXTRA_ENV): irl's plain LDS layout / padded, single-buffered rows
+    "irl_lds2": "",
     "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws,-groups,-dwgap,-rt,-ir,-irl,-pin",
 }
-EXTRA_ENV = {"irl_lds0": {"ZARU_HIP_IRL_LDS": "0"}}  # name -> extra environment
+EXTRA_ENV = {"irl_lds0": {"ZARU_HIP_IRL_LDS": "0"}, "irl_lds2": {"ZARU_HIP_IRL_LDS": "2"}}  # name -> extra env
 
 
 @pytest.fixture(scope="module")

@@ -283,36 +283,73 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
                 const float bb = sW[(t - 1) & 1][IRL_CEC * KK + dc];
 #pragma unroll
                 for (int o = 0; o < RW; ++o) a[o] = bb;
+                if constexpr (LV >= 3) {
+                    // the window rows double-buffered: row ky + 1's reads are issued before row
+                    // ky's FMAs, and each vector is taken whole just before its use (the one
+                    // depthwise wave per SIMD otherwise waits out an LDS latency per row)
+                    constexpr int NR = WWIN / 4;
+                    f32x4 rb[2][NR];
 #pragma unroll
-                for (int ky = 0; ky < K; ++ky) {
-                    const float *row = pe + (dy * S + ky) * PW;
-                    float xw[WWIN];
-                    if constexpr (W64) {
-                        if constexpr (LV == 2) {
+                    for (int e = 0; e < NR; ++e) rb[0][e] = reinterpret_cast<const f32x4 *>(pe + dy * S * PW)[e];
 #pragma unroll
-                            for (int e = 0; e < WWIN / 4; ++e) {
-                                f32x4 v = reinterpret_cast<const f32x4 *>(row)[e];
-                                asm("" : "+v"(v));  // (whole: no narrowed / re-paired reads)
+                    for (int ky = 0; ky < K; ++ky) {
+                        // this row's weights first: LDS returns in order, so waiting for them
+                        // does not wait for the next row's reads issued after them
+                        float wr[K];
 #pragma unroll
-                                for (int i = 0; i < 4; ++i) xw[4 * e + i] = v[i];
+                        for (int kx = 0; kx < K; ++kx) wr[kx] = w[ky * K + kx];
+                        if (ky + 1 < K) {
+#pragma unroll
+                            for (int e = 0; e < NR; ++e)
+                                rb[(ky + 1) & 1][e] = reinterpret_cast<const f32x4 *>(pe + (dy * S + ky + 1) * PW)[e];
+                        }
+                        __builtin_amdgcn_sched_barrier(0);  // (keep the reads ahead of the FMAs)
+                        float xw[WWIN];
+#pragma unroll
+                        for (int e = 0; e < NR; ++e) {
+                            f32x4 v = rb[ky & 1][e];
+                            asm("" : "+v"(v));
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) xw[4 * e + i] = v[i];
+                        }
+#pragma unroll
+                        for (int kx = 0; kx < K; ++kx) {
+#pragma unroll
+                            for (int o = 0; o < RW; ++o) a[o] = __builtin_fmaf(wr[kx], xw[o * S + kx], a[o]);
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int ky = 0; ky < K; ++ky) {
+                        const float *row = pe + (dy * S + ky) * PW;
+                        float xw[WWIN];
+                        if constexpr (W64) {
+                            if constexpr (LV >= 2) {
+#pragma unroll
+                                for (int e = 0; e < WWIN / 4; ++e) {
+                                    f32x4 v = reinterpret_cast<const f32x4 *>(row)[e];
+                                    asm("" : "+v"(v));  // (whole: no narrowed / re-paired reads)
+#pragma unroll
+                                    for (int i = 0; i < 4; ++i) xw[4 * e + i] = v[i];
+                                }
+                            } else {
+#pragma unroll
+                                for (int e = 0; e < WWIN / 2; ++e) {
+                                    const float2 v = reinterpret_cast<const float2 *>(row)[e];
+                                    xw[2 * e] = v.x;
+                                    xw[2 * e + 1] = v.y;
+                                }
                             }
                         } else {
 #pragma unroll
-                            for (int e = 0; e < WWIN / 2; ++e) {
-                                const float2 v = reinterpret_cast<const float2 *>(row)[e];
-                                xw[2 * e] = v.x;
-                                xw[2 * e + 1] = v.y;
-                            }
+                            for (int e = 0; e < (RW - 1) * S + K; ++e) xw[e] = row[e];
                         }
-                    } else {
 #pragma unroll
-                        for (int e = 0; e < (RW - 1) * S + K; ++e) xw[e] = row[e];
-                    }
+                        for (int kx = 0; kx < K; ++kx) {
+                            const float wt = w[ky * K + kx];
 #pragma unroll
-                    for (int kx = 0; kx < K; ++kx) {
-                        const float wt = w[ky * K + kx];
-#pragma unroll
-                        for (int o = 0; o < RW; ++o) a[o] = __builtin_fmaf(wt, xw[o * S + kx], a[o]);
+                            for (int o = 0; o < RW; ++o) a[o] = __builtin_fmaf(wt, xw[o * S + kx], a[o]);
+                        }
                     }
                 }
                 float *dst = sD[(t - 1) & 1] + dc * DCS + dj * NCP + dy * HO + dx0;
@@ -365,11 +402,12 @@ __global__ __launch_bounds__(512) void irl_kernel(const GemmParams E, const DwPw
 int irl_trace_launches = 0;  // (trace builds: the buffer's launch slot of the next irl launch)
 #endif
 
-// ZARU_HIP_IRL_LDS=0 (A/B knob, bitwise neutral): the plain layout everywhere
+// ZARU_HIP_IRL_LDS (A/B knob, bitwise neutral): 0 the plain layout everywhere, 2 the padded one,
+// 3 (default) padded + double-buffered window rows
 int irl_lds_env() {
     static const int v = [] {
         const char *e = std::getenv("ZARU_HIP_IRL_LDS");
-        return e ? (int)std::strtol(e, nullptr, 10) : 2;
+        return e ? (int)std::strtol(e, nullptr, 10) : 3;
     }();
     return v;
 }
@@ -383,7 +421,10 @@ const char *irl_go(const GemmParams &e, const DwPwParams &d, hipStream_t s) {
 #else
 #define IRL_TRACE_PASS
 #endif
-    if (padded && irl_lds_env() != 0)
+    const int lv = irl_lds_env();
+    if (padded && lv >= 3)
+        hipLaunchKernelGGL((irl_kernel<K, HW, S, CX, MP, NI, padded ? 3 : 0>), dim3((N + NI - 1) / NI), dim3(512), 0, s, e, d IRL_TRACE_PASS);
+    else if (padded && lv == 2)
         hipLaunchKernelGGL((irl_kernel<K, HW, S, CX, MP, NI, padded ? 2 : 0>), dim3((N + NI - 1) / NI), dim3(512), 0, s, e, d IRL_TRACE_PASS);
     else hipLaunchKernelGGL((irl_kernel<K, HW, S, CX, MP, NI, 0>), dim3((N + NI - 1) / NI), dim3(512), 0, s, e, d IRL_TRACE_PASS);
     return NI == 1 ? kernel_name("irl_kernel<%d,%d,%d,%d,%d>", K, HW, S, CX, MP)
