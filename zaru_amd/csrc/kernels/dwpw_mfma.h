@@ -728,13 +728,16 @@ const char *dwpw_go(const DwPwParams &p, hipStream_t s) {
     }
     if (const size_t lds = dma_plan<K, S, WM, MTW, 16>(p, &runmax, &bufsz))
         return dma_launch<K, S, WM, MTW, 16>(p, grid, lds, nct, runmax, bufsz, s);
-    if constexpr (K == 5 && S == 2 && MTW >= 4) {
+    if constexpr ((K == 5 && S == 2 && MTW >= 4) || (K == 3 && S == 2 && MTW == 2)) {
         // stride-2 5x5 tiles over large planes whose input runs do not fit two 16-channel
         // buffers: 8-channel chunks.  BlazePalm's 48^2 -> 24^2 block (128 rows): 163 vs 232 us
         // register-staged at 256 frames; its 96^2 -> 48^2 block (64 rows, MTW 2) measured slower
         // (272 vs 259 us), so it keeps the register-staged form (profiles/r05_layers/)
-        if (const size_t lds = dma_plan<K, S, WM, MTW, 8>(p, &runmax, &bufsz))
-            return dma_launch<K, S, WM, MTW, 8>(p, grid, lds, nct, runmax, bufsz, s);
+        // (3x3 stride 2, MTW 2 -- FaceMesh's 48^2 -> 24^2 block: only with form pin, whose
+        // 4-wide tasks read 16-byte windows)
+        if (K == 5 || form_on(FORM_PIN))
+            if (const size_t lds = dma_plan<K, S, WM, MTW, 8>(p, &runmax, &bufsz))
+                return dma_launch<K, S, WM, MTW, 8>(p, grid, lds, nct, runmax, bufsz, s);
     }
     const bool v4 = v4_ok(p);
     if (v4) hipLaunchKernelGGL((dwpw_kernel<K, S, WM, MTW, 1, true>), grid, dim3(256), 0, s, p, nct);
