@@ -51,9 +51,11 @@ SWITCHES = {
     "no_pin": "-pin",
     "irl_lds0": "",  # + ZARU_HIP_IRL_LDS (EXTRA_ENV): irl's plain LDS layout / padded, single-buffered rows
     "irl_lds2": "",
+    "dma_pad": "",  # + ZARU_HIP_DMA_PAD=1: the bank-padded LDS channel stride of the pin layouts
     "all_off": "-dma,-v4,-valu,-valu_db,-rows,-vres,-vstore,-ws,-groups,-dwgap,-rt,-ir,-irl,-pin",
 }
-EXTRA_ENV = {"irl_lds0": {"ZARU_HIP_IRL_LDS": "0"}, "irl_lds2": {"ZARU_HIP_IRL_LDS": "2"}}  # name -> extra env
+EXTRA_ENV = {"irl_lds0": {"ZARU_HIP_IRL_LDS": "0"}, "irl_lds2": {"ZARU_HIP_IRL_LDS": "2"},
+             "dma_pad": {"ZARU_HIP_DMA_PAD": "1"}}  # name -> extra env
 
 
 @pytest.fixture(scope="module")

@@ -679,6 +679,14 @@ static int rt_for(const DwPwParams &p, int bn, int r_hi) {
     return 0;
 }
 
+static bool dma_pad_on() {
+    static const bool v = [] {
+        const char *e = std::getenv("ZARU_HIP_DMA_PAD");
+        return e && std::strtol(e, nullptr, 10) > 0;
+    }();
+    return v;
+}
+
 template <int K, int S, int WM, int MTW, int DFKC, int RT>
 static const char *dma_go(const DwPwParams &p, dim3 grid, size_t lds, int nct, int runmax, int bufsz, hipStream_t s) {
     // form "pin" where the task step RT * S makes 16-byte window reads (ds_read_b128: FaceMesh 24^2
@@ -688,6 +696,20 @@ static const char *dma_go(const DwPwParams &p, dim3 grid, size_t lds, int nct, i
     // (profiles/r06_layers/*_pin_vs_not.txt)
     if constexpr (RT > 0 && (RT * S) % 4 == 0)
         if (form_on(FORM_PIN) && p.in.W % 4 == 0) {
+            // channel stride: a half-wave's b128 groups hold 8 lanes of each of 2 channels (16
+            // tasks per channel) or 4 of each of 4 (8 tasks); with 16-byte-apart lanes they are
+            // conflict-free when consecutive channels sit 0 resp. 32 words apart mod 64
+            // (tools/lds_banks.py).  ZARU_HIP_DMA_PAD=1 pads the stride so: PMC conflicts 1.2-2.9
+            // -> 0.2-0.5 per LDS instruction, but no launch faster and the face line 268 k vs 271 k,
+            // BlazePalm +1.3 % (profiles/r06_layers/*_pinpad_vs_packed.txt) -- off by default
+            constexpr int BN = (4 / WM) * 32, SEGS = BN / RT, TASKS = DFKC * SEGS;
+            constexpr int SPT = SEGS / (TASKS > 256 ? TASKS / 256 : 1), RES = SPT == 16 ? 0 : SPT == 8 ? 32 : -1;
+            if constexpr (RES >= 0)
+                if (dma_pad_on()) {
+                    int rm = runmax, bz = 0;
+                    while (rm % 64 != RES) rm += 4;
+                    if (const size_t l = dma_lds<K, WM, MTW, DFKC>(rm, &bz)) runmax = rm, bufsz = bz, lds = l;
+                }
             hipLaunchKernelGGL((dwpw_dma_pin_kernel<K, S, WM, MTW, DFKC, RT>), grid, dim3(256), lds, s, p, nct, runmax, bufsz);
             return kernel_name("dwpw_dma_pin_kernel<%d,%d,%d,%d,%d,%d>", K, S, WM, MTW, DFKC, RT);
         }
