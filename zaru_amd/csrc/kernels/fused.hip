@@ -555,7 +555,15 @@ const char *dwpw_valu_go(const DwPwParams &p, hipStream_t s) {
     const int vres = vres_mode(p, S, CO);
     const bool db = form_on(FORM_VALU_DB) && (CO == 16 || CO == 32 || (CO == 48 && (S == 2 || vres))) &&
                     2 * sizeof(float) * (size_t)buf_of(4) <= 64 * 1024;
-    const bool small = db && !(CO == 32 && fit8);
+    // 16 channels from >= 32 inputs at >= 96-wide planes (BlazeFace full range's 96^2 32 -> 8):
+    // 8-channel chunks too, half the DMA round trips per tile (122 / 119 -> 117 / 114 us at 171
+    // images; the hand network's 112^2 24 -> 16 lost 240 -> 282 us, its larger buffers halving the
+    // workgroups per CU: profiles/r06_layers/*_valu16vf8_vs_4.txt).  ZARU_HIP_VALU16_VF8=0: 4.
+    static const bool v16 = [] {
+        const char *e = std::getenv("ZARU_HIP_VALU16_VF8");
+        return !e || std::strtol(e, nullptr, 10) != 0;
+    }();
+    const bool small = db && !((CO == 32 || (CO == 16 && v16 && p.in.W >= 96 && p.g.K >= 32)) && fit8);
     const int vf = small ? 4 : VFKC;
     const int bufsz = buf_of(vf);
     dim3 grid((ntiles + 7) / 8 * 8);
